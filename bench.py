@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""bench.py -- hash-join throughput on MI355X (BASELINE.json metric).
+
+Metric: probed tuples/s (+ joined rows/s), |R| = |S| = 2^28 int64 key +
+int64 payload, PK-FK synthetic relations (SURVEY 8(d) C3 shape: R keys
+unique, every S row matches exactly one R row).  One step = one complete
+join of the whole relations with inputs resident in HBM:
+
+  N = 1 : table init + build + probe (one GPU holds everything: ~22 GiB)
+  N > 1 : radix partition R and S -> RCCL all-to-all of 16-B tuples ->
+          local init + build + probe (strong scaling: the GLOBAL relations
+          stay 2^28 x 2^28; each rank generates its 1/N slice)
+
+value = |S| / (time per step), the whole job over all ranks (max over ranks).
+Launch:  python bench.py [--gpus 1 --steps K --warmup W]
+         python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mlir-hashjoin_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (log2 |R|, log2 |S|, distribution, description)
+    "C3": (28, 28, "pkfk", "PK-FK |R|=|S|=2^28 int64 key+payload, match fraction 1"),
+    "C1": (26, 26, "pkfk", "PK-FK |R|=|S|=2^26 int64 key+payload, match fraction 1"),
+    "C1-ref": (26, 26, "uniform", "uniform keys in [1,2^30] both sides, |R|=|S|=2^26 int64"),
+    "C2": (20, 30, "pkfk", "PK-FK |R|=2^20 build, |S|=2^30 probe, int64"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-log2", type=int, default=22)
+    ap.add_argument("--verify", action="store_true", help="check the last step's output properties")
+    return ap.parse_args()
+
+
+def cpu_baseline(seed, log2n, threads):
+    """The reference's join_v2 (chained table, key urem H with H = |R|/100 as
+    join-performances.md:3,8, count -> block scan -> staged probe) restated on
+    host threads (oracle/, test infrastructure), timed on a bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import pyoracle as O
+    n = 1 << log2n
+    rk, rp, sk, sp = O.gen_pkfk_i64(seed, n, n)
+    H = max(1, n // 100)
+    O.chained_join_i64_omp(rk[:4096], rp[:4096], sk[:4096], sp[:4096], 41, threads)   # warm the pool
+    t0 = time.perf_counter()
+    m, ph = O.chained_join_i64_omp(rk, rp, sk, sp, H, threads)
+    dt = time.perf_counter() - t0
+    assert m == n, (m, n)
+    return {"value": n / dt, "unit": "probe tuples/s", "cores": threads, "kind": "port",
+            "sample": f"|R|=|S|=2^{log2n} PK-FK int64, H=|R|/100 (reference ratio), join_v2 restated "
+                      f"(oracle/hj_oracle.c) on {threads} host threads; {dt:.2f} s "
+                      f"(init {ph[0]:.2f} / build {ph[1]:.2f} / count {ph[2]:.2f} / probe {ph[3]:.2f} s)"}
+
+
+def pmc_traffic(config, n_gpus):
+    """HBM bytes per probe launch from the committed rocprofv3 PMC summary of
+    this workload (profiles/pmc_latest.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        e = d.get(f"{config}/n{n_gpus}")
+        return None if e is None else e.get("probe_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import hashjoin
+    from hashjoin.dist import distributed_join
+
+    lr, ls, distn, desc = CONFIGS[a.config]
+    NR, NS = 1 << lr, 1 << ls
+    r0, nr = rank * NR // world, (rank + 1) * NR // world - rank * NR // world
+    s0, ns = rank * NS // world, (rank + 1) * NS // world - rank * NS // world
+    if distn == "pkfk":
+        rk, rp, sk, sp = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, ns)
+    else:
+        rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)
+        sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 1 << 30, ns, i0=s0)
+    hj = hashjoin.HashJoin(local)
+    expect_m = NS if distn == "pkfk" else None
+    torch.cuda.synchronize()
+
+    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "partition+exchange": 0.0}
+    last = {}
+
+    if world == 1:
+        hj.allocate_hash_table(NR, 64)
+        cap = NS if distn == "pkfk" else int(NR * NS / (1 << 30) * 1.1) + 4096
+        out_r = torch.empty(cap, dtype=torch.int64, device="cuda")
+        out_s = torch.empty_like(out_r)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        hj.set_timing(True)
+
+        def step(acc):
+            hj.build_table(rk, rp)
+            hj.probe_relation(sk, sp, out_r, out_s, count=cnt)
+            t = hj.last_timing()          # synchronises: the step ends with M known on the host
+            if acc:
+                for k in ("init", "build", "probe"):
+                    phases[k] += t[k]
+            last["m"] = int(cnt.item())
+    else:
+        # strong scaling over the GLOBAL relations; output stays distributed
+        hj.allocate_hash_table(2 * nr, 64)
+
+        def step(acc):
+            ev = {}
+            o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev)
+            ev["probed"].synchronize()
+            if acc:
+                phases["partition+exchange"] += ev["start"].elapsed_time(ev["exchanged"])
+                phases["build"] += ev["exchanged"].elapsed_time(ev["built"])
+                phases["probe"] += ev["built"].elapsed_time(ev["probed"])
+            last["m"] = o_r.numel()
+            last["out"] = (o_r, o_s)
+
+    for _ in range(a.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    m_local = last["m"]
+    if world > 1:
+        tt = torch.tensor([elapsed, float(m_local)], dtype=torch.float64, device="cuda")
+        mx = tt.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0].item()); m_total = int(sm[1].item())
+    else:
+        m_total = m_local
+    if expect_m is not None and m_total != expect_m:
+        raise SystemExit(f"join produced {m_total} rows, expected {expect_m}")
+
+    if a.verify and world == 1:
+        o_r, o_s = out_r[:m_local], out_s[:m_local]
+        assert bool((rk[o_r] == sk[o_s]).all()), "non-matching pair in output"
+
+    ms = elapsed * 1000.0 / a.steps
+    value = NS / (ms / 1000.0)
+    ph = {k: round(v / a.steps, 4) for k, v in phases.items() if v > 0}
+
+    # roofline of the dominant kernel (probe): algorithmic bytes per launch =
+    # |S_local| x (16 B stream S + 16 B one slot read) + M_local x 16 B output
+    # (SURVEY 8(d)), over the probe kernel's average HIP-event duration.
+    probe_ms = phases["probe"] / a.steps
+    probe_bytes = ns * 32 + m_local * 16
+    achieved = probe_bytes / (probe_ms / 1000.0) / 1e9 if probe_ms > 0 else None
+    build_ms = phases["build"] / a.steps
+    line = {
+        "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
+        "value": round(value, 1),
+        "unit": "probe tuples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (counter-based PK-FK generator, seed 0x5EED, generated on device)",
+        "config": {"workload": f"{a.config}: {desc}", "R_rows": NR, "S_rows": NS, "key": "int64",
+                   "payload": "int64", "distribution": distn,
+                   "parallelism": "single GPU" if world == 1 else f"radix-partitioned x{world}, RCCL all-to-all"},
+        "joined_rows_per_sec": round(m_total / (ms / 1000.0), 1),
+        "result_rows": m_total,
+        "phase_ms": ph,
+        "roofline": {
+            "kernel": "k_probe (hj_kernels.hip)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": pmc_traffic(a.config, world),
+            "algorithmic_bytes_per_launch": probe_bytes,
+            "avg_launch_ms": round(probe_ms, 4),
+        },
+        "build_roofline": {
+            "kernel": "k_build",
+            "achieved": round(nr * 32 / (build_ms / 1000.0) / 1e9, 1) if build_ms > 0 else None,
+            "unit": "GB/s", "algorithmic_bytes_per_launch": nr * 32, "avg_launch_ms": round(build_ms, 4),
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        line["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_sample_log2, threads)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    hj.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

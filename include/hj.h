@@ -1,0 +1,176 @@
+/*
+ * hj.h -- C ABI of the MI355X-native hash-join operator (libhj.so).
+ *
+ * Drop-in boundary for the reference's join program (deveshv-99/mlir-HashJoin,
+ * SURVEY 8(b)).  Three layers, all plain C (pointers + sizes, no torch types):
+ *
+ *  1. Host memref ABI.  The reference's host functions take ranked 1-D
+ *     memrefs, which MLIR's -finalize-memref-to-llvm / -convert-func-to-llvm
+ *     expand into five scalars (allocated, aligned, offset, size, stride);
+ *     see join_v1.ll:1262-1265 and shared_stuff/shared.cpp:35,59,83,129-132.
+ *     hj_count_* / hj_probe_* use exactly that expansion, so a .mlir module
+ *     declares them `func.func private` and links libhj.so through
+ *     mlir-cpu-runner --shared-libs (run_test.sh:33), the way it links
+ *     shared.so today (join_v1.mlir:651-658).
+ *
+ *  2. MLIR C-interface (`llvm.emit_c_interface`) one-memref-out joins:
+ *     _mlir_ciface_hj_join_*(result*, R*, S*) -- the "two-memref-in /
+ *     one-memref-out" entry point of north_star.  The result buffer is
+ *     malloc'ed (allocated == aligned) so MLIR's memref.dealloc (free) or
+ *     hj_free_result() releases it.
+ *
+ *  3. Device-resident phases (hj_dev_*): the hot path.  Inputs and outputs
+ *     are device pointers, every call is asynchronous on the given HIP stream
+ *     (NULL = default stream) and launches kernels only (no allocation, no
+ *     synchronisation) once hj_ctx_reserve() has sized the workspace, so the
+ *     sequence can be captured into a hipGraph.
+ *
+ * Semantics (all layers): an equi-join of R and S on the key column; the
+ * output is the multiset {(R.pay[i], S.pay[j]) : R.key[i] == S.key[j]} --
+ * every pair, duplicates on either side included, exactly the nested-loop
+ * definition of shared_stuff/shared.cpp:154-165 (payload = row id in the
+ * reference types).  Row order is unspecified (the reference's is decided by
+ * atomics too); compare after sorting, as shared.cpp:168-171 does.
+ *
+ * Errors: functions returning int return HJ_OK (0) or a negative HJ_ERR_*;
+ * hj_last_error() gives "file:line: message" of the last failure on this
+ * thread.  The reference has no error channel besides check()'s 1/0/-1
+ * (shared.cpp:158-171).
+ */
+#ifndef HJ_H_
+#define HJ_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HJ_ABI_VERSION 1
+
+#define HJ_OK 0
+#define HJ_ERR_ARG (-1)      /* bad argument / size mismatch */
+#define HJ_ERR_HIP (-2)      /* HIP runtime error (see hj_last_error) */
+#define HJ_ERR_NOMEM (-3)    /* device or host allocation failed */
+#define HJ_ERR_STATE (-4)    /* call order: probe before build, wrong layout */
+#define HJ_ERR_CAPACITY (-5) /* output memref smaller than the join result */
+
+typedef struct hj_ctx hj_ctx;
+
+int hj_abi_version(void);
+const char *hj_last_error(void);
+
+/* ------------------------------------------------------------------ context
+ * One context = one device + its hash-table workspace.  Replaces the
+ * reference's @allocateHashTable (join_v2.mlir:25-39: gpu.alloc of heads and
+ * linked list) -- allocation is hoisted out of the per-join path. */
+hj_ctx *hj_ctx_create(int device);
+void hj_ctx_destroy(hj_ctx *ctx);
+/* Size the workspace for builds of up to max_build_rows rows with 32- or
+ * 64-bit keys (key_bits = 32 | 64). */
+int hj_ctx_reserve(hj_ctx *ctx, int64_t max_build_rows, int key_bits);
+/* Slot capacity of the current table (power of two, >= 2 x build rows). */
+int64_t hj_ctx_table_capacity(const hj_ctx *ctx);
+/* 1 if the last build saw a duplicate key, 0 if not (synchronises). */
+int hj_ctx_build_has_duplicates(hj_ctx *ctx);
+/* Per-phase kernel timing with HIP events on the caller's stream. */
+int hj_ctx_set_timing(hj_ctx *ctx, int enable);
+/* ms of the last init, build, probe/count and partition launches (synchronises). */
+int hj_ctx_last_timing(hj_ctx *ctx, float ms[4]);
+
+/* ------------------------------------------------------------ device phases
+ * build:  @initializeHashTable + @buildTable   (join_v2.mlir:54-108)
+ * count:  @countRows                           (join_v2.mlir:110-147)
+ * probe:  @probeRelation                       (join_v2.mlir:149-199)
+ * d_count (device uint64): set to M, the exact number of result rows, even
+ * when M > out_cap (rows past out_cap are dropped; re-run with a larger
+ * output).  The counter is zeroed by the call. */
+
+/* 64-bit key / 64-bit payload column pairs (north_star types). */
+int hj_dev_build_i64(hj_ctx *ctx, const int64_t *rkey, const int64_t *rpay, int64_t n, void *stream);
+int hj_dev_count_i64(hj_ctx *ctx, const int64_t *skey, int64_t n, uint64_t *d_count, void *stream);
+int hj_dev_probe_i64(hj_ctx *ctx, const int64_t *skey, const int64_t *spay, int64_t n,
+                     int64_t *out_r, int64_t *out_s, int64_t out_cap, uint64_t *d_count, void *stream);
+/* Same with rows as packed 16-B {key, payload} tuples (the exchange format). */
+int hj_dev_build_tuples_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n, void *stream);
+int hj_dev_probe_tuples_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n,
+                            int64_t *out_r, int64_t *out_s, int64_t out_cap, uint64_t *d_count, void *stream);
+
+/* Reference types: i32 keys, payload = row id (global thread index in
+ * join_v1.mlir:255), (rowR, rowS) i32 output (join_v1.mlir:604-605).
+ * row_base is added to row ids (0 for the reference). */
+int hj_dev_build_i32(hj_ctx *ctx, const int32_t *rkey, int64_t n, int64_t row_base, void *stream);
+int hj_dev_count_i32(hj_ctx *ctx, const int32_t *skey, int64_t n, uint64_t *d_count, void *stream);
+int hj_dev_probe_i32(hj_ctx *ctx, const int32_t *skey, int64_t n, int64_t row_base,
+                     int32_t *out_r, int32_t *out_s, int64_t out_cap, uint64_t *d_count, void *stream);
+
+/* Radix partition of rows into nparts groups by a key hash independent of
+ * the table's slot hash: out_tuples (2*n int64) receives packed {key, pay}
+ * tuples grouped by partition in order 0..nparts-1, d_counts (nparts uint64)
+ * the group sizes.  Multi-GPU routing step (north_star: "build-side
+ * partitioning ... probe tuples routed by the same radix"). */
+int hj_dev_partition_i64(hj_ctx *ctx, const int64_t *key, const int64_t *pay, int64_t n, int nparts,
+                         int64_t *out_tuples, uint64_t *d_counts, void *stream);
+int hj_dev_partition_tuples_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n, int nparts,
+                                int64_t *out_tuples, uint64_t *d_counts, void *stream);
+/* Owning partition of one key (host-side, same function as the kernels). */
+int hj_partition_of(int64_t key, int nparts);
+
+/* Deterministic synthetic relations (counter-based, so any slice of a
+ * global relation can be generated independently on any GPU). */
+int hj_dev_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_threshold,
+                        int64_t r0, int64_t nr, int64_t *rkey, int64_t *rpay,
+                        int64_t s0, int64_t ns, int64_t *skey, int64_t *spay, void *stream);
+int hj_dev_gen_uniform_i64(uint64_t seed, uint64_t stream_id, int64_t lo, int64_t hi,
+                           int64_t i0, int64_t n, int64_t *key, int64_t *pay, void *stream);
+int hj_dev_gen_uniform_i32(uint64_t seed, uint64_t stream_id, int32_t lo, int32_t hi,
+                           int64_t i0, int64_t n, int32_t *key, void *stream);
+
+/* ------------------------------------------------------- host memref ABI
+ * Two-phase, reference-shaped (mirrors @countRows -> alloc -> @probeRelation,
+ * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion.  Both calls
+ * are self-contained (copy in, build, probe, copy out); offset and stride of
+ * every memref are honoured.  hj_probe_* returns HJ_OK, or HJ_ERR_CAPACITY
+ * when the output memrefs' size differs from the join's row count. */
+int64_t hj_count_i32(int32_t *r_alloc, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride,
+                     int32_t *s_alloc, int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride);
+int32_t hj_probe_i32(int32_t *r_alloc, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride,
+                     int32_t *s_alloc, int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride,
+                     int32_t *or_alloc, int32_t *or_align, int64_t or_off, int64_t or_size, int64_t or_stride,
+                     int32_t *os_alloc, int32_t *os_align, int64_t os_off, int64_t os_size, int64_t os_stride);
+/* int64 key/payload column pairs (Rkey, Rpay, Skey, Spay). */
+int64_t hj_count_i64(int64_t *rk_alloc, int64_t *rk_align, int64_t rk_off, int64_t rk_size, int64_t rk_stride,
+                     int64_t *rp_alloc, int64_t *rp_align, int64_t rp_off, int64_t rp_size, int64_t rp_stride,
+                     int64_t *sk_alloc, int64_t *sk_align, int64_t sk_off, int64_t sk_size, int64_t sk_stride,
+                     int64_t *sp_alloc, int64_t *sp_align, int64_t sp_off, int64_t sp_size, int64_t sp_stride);
+int32_t hj_probe_i64(int64_t *rk_alloc, int64_t *rk_align, int64_t rk_off, int64_t rk_size, int64_t rk_stride,
+                     int64_t *rp_alloc, int64_t *rp_align, int64_t rp_off, int64_t rp_size, int64_t rp_stride,
+                     int64_t *sk_alloc, int64_t *sk_align, int64_t sk_off, int64_t sk_size, int64_t sk_stride,
+                     int64_t *sp_alloc, int64_t *sp_align, int64_t sp_off, int64_t sp_size, int64_t sp_stride,
+                     int64_t *or_alloc, int64_t *or_align, int64_t or_off, int64_t or_size, int64_t or_stride,
+                     int64_t *os_alloc, int64_t *os_align, int64_t os_off, int64_t os_size, int64_t os_stride);
+
+/* ------------------------------------------------------ MLIR C-interface
+ * Descriptor structs of memref<?xT> / memref<?x2xT> (MLIR's StridedMemRefType
+ * layout: allocated, aligned, offset, sizes[rank], strides[rank]). */
+typedef struct { int32_t *allocated; int32_t *aligned; int64_t offset; int64_t sizes[1]; int64_t strides[1]; } hj_memref1_i32;
+typedef struct { int64_t *allocated; int64_t *aligned; int64_t offset; int64_t sizes[1]; int64_t strides[1]; } hj_memref1_i64;
+typedef struct { int32_t *allocated; int32_t *aligned; int64_t offset; int64_t sizes[2]; int64_t strides[2]; } hj_memref2_i32;
+typedef struct { int64_t *allocated; int64_t *aligned; int64_t offset; int64_t sizes[2]; int64_t strides[2]; } hj_memref2_i64;
+
+/* memref<?xi32> R, S -> memref<?x2xi32> rows (rowR, rowS): the reference's
+ * whole @main join (join_v2.mlir:607-730) as one call. */
+void _mlir_ciface_hj_join_i32(hj_memref2_i32 *result, hj_memref1_i32 *r, hj_memref1_i32 *s);
+/* memref<?xi64> R, S keys (payload = row id) -> memref<?x2xi64> (rowR, rowS). */
+void _mlir_ciface_hj_join_i64(hj_memref2_i64 *result, hj_memref1_i64 *r, hj_memref1_i64 *s);
+/* key/payload column pairs -> memref<?x2xi64> (R.pay, S.pay). */
+void _mlir_ciface_hj_join_kp_i64(hj_memref2_i64 *result, hj_memref1_i64 *rkey, hj_memref1_i64 *rpay,
+                                 hj_memref1_i64 *skey, hj_memref1_i64 *spay);
+/* Release a result buffer of the ciface joins (== free(allocated)). */
+void hj_free_result(void *allocated);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HJ_H_ */

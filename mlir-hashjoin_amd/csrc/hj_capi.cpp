@@ -1,0 +1,706 @@
+// hj_capi.cpp -- the C ABI of libhj.so (declared in include/hj.h).
+//
+// Host side of the join, C++ over HIP.  It replaces the reference's host
+// functions inside join_v1.mlir / join_v2.mlir (@allocateHashTable,
+// @initializeHashTable, @buildTable, @countRows, @probeRelation: join_v2.mlir:
+// 25-199) and the @main data path (:607-730).  The reference lowers every
+// gpu.launch_func to stream create -> module load -> launch -> unload ->
+// synchronize -> destroy (join_v2.ll:133-172); here one context keeps its
+// workspace and every device phase is an asynchronous launch on the caller's
+// stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hj.h"
+#include "hj_internal.h"
+
+using hj::kNarrow;
+using hj::kWide;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *file, int line, const std::string &msg) {
+    g_err = std::string(file) + ":" + std::to_string(line) + ": " + msg;
+    if (code == HJ_ERR_HIP || code == HJ_ERR_NOMEM) std::fprintf(stderr, "hj: %s\n", g_err.c_str());
+    return code;
+}
+
+#define HJ_FAIL(code, msg) return fail((code), __FILE__, __LINE__, (msg))
+#define HJ_HIP(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail(HJ_ERR_HIP, __FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define HJ_TRY(expr)              \
+    do {                          \
+        int r_ = (expr);          \
+        if (r_ != HJ_OK) return r_; \
+    } while (0)
+
+int ceil_log2(unsigned long long x) {
+    int b = 0;
+    while ((1ull << b) < x) ++b;
+    return b;
+}
+
+// Table capacity for n build rows: power of two >= 2n (load factor <= 0.5),
+// at least 16 slots.
+int table_bits(int64_t n) {
+    const unsigned long long want = 2ull * (unsigned long long)(n > 0 ? n : 1);
+    int b = ceil_log2(want);
+    return b < 4 ? 4 : b;
+}
+
+enum Ev { kEvInit0, kEvInit1, kEvBuild1, kEvProbe0, kEvProbe1, kEvPart0, kEvPart1, kEvCount };
+
+}  // namespace
+
+struct hj_ctx {
+    int device = 0;
+    void *table = nullptr;
+    size_t table_bytes = 0;
+    unsigned long long *side = nullptr;   // wide-layout side list (INT64_MIN keys)
+    size_t side_rows = 0;
+    unsigned long long *meta = nullptr;   // [0] side count, [1] dup flag, [8..] partition cursors
+    size_t meta_words = 0;
+    // current table
+    int layout = -1;
+    int bits = 0;
+    int64_t n_build = 0;
+    // timing
+    bool timing = false;
+    bool ev_ready = false;
+    hipEvent_t ev[kEvCount];
+    bool rec[4] = {false, false, false, false};
+    // host memref path
+    hipStream_t host_stream = nullptr;
+    void *dbuf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t dbuf_bytes[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long *dcount = nullptr;
+};
+
+namespace {
+
+int set_device(hj_ctx *c) {
+    HJ_HIP(hipSetDevice(c->device));
+    return HJ_OK;
+}
+
+int ensure_meta(hj_ctx *c, size_t words) {
+    if (c->meta_words >= words) return HJ_OK;
+    if (c->meta) HJ_HIP(hipFree(c->meta));
+    c->meta = nullptr;
+    size_t w = words < 64 ? 64 : words;
+    if (hipMalloc(&c->meta, w * sizeof(unsigned long long)) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc meta");
+    HJ_HIP(hipMemset(c->meta, 0, w * sizeof(unsigned long long)));
+    c->meta_words = w;
+    return HJ_OK;
+}
+
+int ensure_table(hj_ctx *c, int64_t n, int layout) {
+    const int bits = table_bits(n);
+    const size_t need = (size_t(1) << bits) * (layout == kWide ? 16 : 8);
+    if (c->table_bytes < need) {
+        if (c->table) HJ_HIP(hipFree(c->table));
+        c->table = nullptr;
+        c->table_bytes = 0;
+        if (hipMalloc(&c->table, need) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc table " + std::to_string(need));
+        c->table_bytes = need;
+    }
+    if (layout == kWide && c->side_rows < (size_t)(n > 0 ? n : 1)) {
+        if (c->side) HJ_HIP(hipFree(c->side));
+        c->side = nullptr;
+        const size_t rows = (size_t)(n > 0 ? n : 1);
+        if (hipMalloc(&c->side, rows * 8) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc side list");
+        c->side_rows = rows;
+    }
+    return ensure_meta(c, 64);
+}
+
+hj::TableDev table_dev(const hj_ctx *c) {
+    hj::TableDev t;
+    t.slots = c->table;
+    t.mask = (1ull << c->bits) - 1ull;
+    t.shift = 64 - c->bits;
+    t.side = c->side;
+    t.meta = c->meta;
+    return t;
+}
+
+void record(hj_ctx *c, int ev, hipStream_t st) {
+    if (c->timing && c->ev_ready) (void)hipEventRecord(c->ev[ev], st);
+}
+
+int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (src.n < 0 || (src.n > 0 && !src.key) || (src.form == hj::kCols64 && src.n > 0 && !src.pay))
+        HJ_FAIL(HJ_ERR_ARG, "bad build relation");
+    if (layout == kNarrow && src.n > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids: build side must have < 2^31 rows");
+    HJ_TRY(set_device(c));
+    HJ_TRY(ensure_table(c, src.n, layout));
+    c->layout = layout;
+    c->bits = table_bits(src.n);
+    c->n_build = src.n;
+    const hj::TableDev t = table_dev(c);
+    record(c, kEvInit0, st);
+    HJ_HIP(hj::launch_init(t, layout, 1ull << c->bits, st));
+    record(c, kEvInit1, st);
+    HJ_HIP(hj::launch_build(t, layout, src, st));
+    record(c, kEvBuild1, st);
+    c->rec[0] = c->rec[1] = c->timing;
+    return HJ_OK;
+}
+
+int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *out_s, int64_t cap,
+             uint64_t *d_count, bool count_only, hipStream_t st) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (c->layout != layout) HJ_FAIL(HJ_ERR_STATE, "probe without a matching build");
+    if (!d_count) HJ_FAIL(HJ_ERR_ARG, "null count pointer");
+    if (src.n < 0 || (src.n > 0 && !src.key)) HJ_FAIL(HJ_ERR_ARG, "bad probe relation");
+    if (!count_only && (cap < 0 || (cap > 0 && (!out_r || !out_s)))) HJ_FAIL(HJ_ERR_ARG, "bad output");
+    HJ_TRY(set_device(c));
+    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+    hj::OutDev out;
+    out.r = out_r;
+    out.s = out_s;
+    out.cap = count_only ? 0 : cap;
+    out.counter = (unsigned long long *)d_count;
+    record(c, kEvProbe0, st);
+    HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, st));
+    record(c, kEvProbe1, st);
+    c->rec[2] = c->timing;
+    return HJ_OK;
+}
+
+int do_partition(hj_ctx *c, const hj::SrcDev &src, int nparts, int64_t *out, uint64_t *d_counts, hipStream_t st) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (nparts < 1 || nparts > 65536) HJ_FAIL(HJ_ERR_ARG, "nparts must be in [1, 65536]");
+    if (src.n < 0 || (src.n > 0 && (!src.key || !out))) HJ_FAIL(HJ_ERR_ARG, "bad partition input");
+    if (!d_counts) HJ_FAIL(HJ_ERR_ARG, "null counts");
+    HJ_TRY(set_device(c));
+    HJ_TRY(ensure_meta(c, 8 + (size_t)nparts));
+    record(c, kEvPart0, st);
+    HJ_HIP(hj::launch_partition(src, nparts, out, (unsigned long long *)d_counts, c->meta + 8, st));
+    record(c, kEvPart1, st);
+    c->rec[3] = c->timing;
+    return HJ_OK;
+}
+
+hj::SrcDev src_cols64(const int64_t *k, const int64_t *p, int64_t n) {
+    hj::SrcDev s;
+    s.key = k;
+    s.pay = p;
+    s.n = n;
+    s.row_base = 0;
+    s.form = hj::kCols64;
+    return s;
+}
+hj::SrcDev src_packed(const int64_t *t, int64_t n) {
+    hj::SrcDev s;
+    s.key = t;
+    s.pay = nullptr;
+    s.n = n;
+    s.row_base = 0;
+    s.form = hj::kPacked64;
+    return s;
+}
+hj::SrcDev src_col32(const int32_t *k, int64_t n, int64_t row_base) {
+    hj::SrcDev s;
+    s.key = k;
+    s.pay = nullptr;
+    s.n = n;
+    s.row_base = row_base;
+    s.form = hj::kCol32;
+    return s;
+}
+
+// ---------------------------------------------------------------- host path
+std::mutex g_default_mu;
+std::map<int, hj_ctx *> g_default;
+
+hj_ctx *default_ctx() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    auto it = g_default.find(dev);
+    if (it != g_default.end()) return it->second;
+    hj_ctx *c = hj_ctx_create(dev);
+    if (c) g_default[dev] = c;
+    return c;
+}
+
+int dbuf(hj_ctx *c, int i, size_t bytes, void **p) {
+    if (bytes == 0) bytes = 16;
+    if (c->dbuf_bytes[i] < bytes) {
+        if (c->dbuf[i]) HJ_HIP(hipFree(c->dbuf[i]));
+        c->dbuf[i] = nullptr;
+        c->dbuf_bytes[i] = 0;
+        if (hipMalloc(&c->dbuf[i], bytes) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc staging");
+        c->dbuf_bytes[i] = bytes;
+    }
+    *p = c->dbuf[i];
+    return HJ_OK;
+}
+
+// Copy a strided host memref (aligned + offset, size, stride) into device
+// buffer `dst` (contiguous).  shared.cpp reads through the aligned pointer
+// (shared.cpp:40, :67, :148); we additionally honour offset and stride.
+template <class T>
+int upload(void *dst, const T *aligned, int64_t off, int64_t size, int64_t stride, hipStream_t st) {
+    if (size <= 0) return HJ_OK;
+    if (!aligned) HJ_FAIL(HJ_ERR_ARG, "null memref");
+    const T *base = aligned + off;
+    if (stride == 1) {
+        HJ_HIP(hipMemcpyAsync(dst, base, sizeof(T) * (size_t)size, hipMemcpyHostToDevice, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        return HJ_OK;
+    }
+    std::vector<T> tmp((size_t)size);
+    for (int64_t i = 0; i < size; ++i) tmp[(size_t)i] = base[i * stride];
+    HJ_HIP(hipMemcpyAsync(dst, tmp.data(), sizeof(T) * (size_t)size, hipMemcpyHostToDevice, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    return HJ_OK;
+}
+
+int host_stream(hj_ctx *c) {
+    if (!c->host_stream) HJ_HIP(hipStreamCreateWithFlags(&c->host_stream, hipStreamNonBlocking));
+    if (!c->dcount) {
+        if (hipMalloc(&c->dcount, 64) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc counter");
+    }
+    return HJ_OK;
+}
+
+// Full host-memref join, i32 reference types (narrow table).  Result rows go
+// to the device buffers dbuf[2], dbuf[3]; *m receives M.
+int host_join_i32(hj_ctx *c, const int32_t *r, int64_t r_off, int64_t nr, int64_t r_stride,
+                  const int32_t *s, int64_t s_off, int64_t ns, int64_t s_stride, bool count_only,
+                  int64_t *m, void **d_or, void **d_os) {
+    if (nr < 0 || ns < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
+    HJ_TRY(set_device(c));
+    HJ_TRY(host_stream(c));
+    hipStream_t st = c->host_stream;
+    void *dr, *ds;
+    HJ_TRY(dbuf(c, 0, sizeof(int32_t) * (size_t)nr, &dr));
+    HJ_TRY(dbuf(c, 1, sizeof(int32_t) * (size_t)ns, &ds));
+    HJ_TRY(upload<int32_t>(dr, r, r_off, nr, r_stride, st));
+    HJ_TRY(upload<int32_t>(ds, s, s_off, ns, s_stride, st));
+    HJ_TRY(do_build(c, kNarrow, src_col32((const int32_t *)dr, nr, 0), st));
+    const hj::SrcDev probe = src_col32((const int32_t *)ds, ns, 0);
+    uint64_t cnt = 0;
+    if (count_only) {
+        HJ_TRY(do_probe(c, kNarrow, probe, nullptr, nullptr, 0, (uint64_t *)c->dcount, true, st));
+        HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        *m = (int64_t)cnt;
+        return HJ_OK;
+    }
+    int64_t cap = ns > 0 ? ns : 1;   // optimistic: a key join usually yields <= |S| rows
+    for (int pass = 0; pass < 2; ++pass) {
+        HJ_TRY(dbuf(c, 2, sizeof(int32_t) * (size_t)cap, d_or));
+        HJ_TRY(dbuf(c, 3, sizeof(int32_t) * (size_t)cap, d_os));
+        HJ_TRY(do_probe(c, kNarrow, probe, *d_or, *d_os, cap, (uint64_t *)c->dcount, false, st));
+        HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        if ((int64_t)cnt <= cap) break;
+        cap = (int64_t)cnt;   // exact M known: second pass fits
+    }
+    *m = (int64_t)cnt;
+    return HJ_OK;
+}
+
+// Full host-memref join over int64 columns; rpay / spay may be null (payload
+// = row id, as the reference's rowId column, join_v1.mlir:255).
+int host_join_i64(hj_ctx *c, const int64_t *rk, int64_t rk_off, int64_t rk_stride, const int64_t *rp,
+                  int64_t rp_off, int64_t rp_stride, int64_t nr, const int64_t *sk, int64_t sk_off,
+                  int64_t sk_stride, const int64_t *sp, int64_t sp_off, int64_t sp_stride, int64_t ns,
+                  bool count_only, int64_t *m, void **d_or, void **d_os) {
+    if (nr < 0 || ns < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
+    HJ_TRY(set_device(c));
+    HJ_TRY(host_stream(c));
+    hipStream_t st = c->host_stream;
+    void *drk, *drp, *dsk, *dsp;
+    HJ_TRY(dbuf(c, 0, 16 * (size_t)nr, &drk));   // key column then payload column
+    HJ_TRY(dbuf(c, 1, 16 * (size_t)ns, &dsk));
+    drp = (char *)drk + 8 * (size_t)nr;
+    dsp = (char *)dsk + 8 * (size_t)ns;
+    HJ_TRY(upload<int64_t>(drk, rk, rk_off, nr, rk_stride, st));
+    HJ_TRY(upload<int64_t>(dsk, sk, sk_off, ns, sk_stride, st));
+    if (rp) {
+        HJ_TRY(upload<int64_t>(drp, rp, rp_off, nr, rp_stride, st));
+    } else if (nr > 0) {
+        std::vector<int64_t> iota((size_t)nr);
+        for (int64_t i = 0; i < nr; ++i) iota[(size_t)i] = i;
+        HJ_TRY(upload<int64_t>(drp, iota.data(), 0, nr, 1, st));
+    }
+    if (sp) {
+        HJ_TRY(upload<int64_t>(dsp, sp, sp_off, ns, sp_stride, st));
+    } else if (ns > 0) {
+        std::vector<int64_t> iota((size_t)ns);
+        for (int64_t i = 0; i < ns; ++i) iota[(size_t)i] = i;
+        HJ_TRY(upload<int64_t>(dsp, iota.data(), 0, ns, 1, st));
+    }
+    HJ_TRY(do_build(c, kWide, src_cols64((const int64_t *)drk, (const int64_t *)drp, nr), st));
+    const hj::SrcDev probe = src_cols64((const int64_t *)dsk, (const int64_t *)dsp, ns);
+    uint64_t cnt = 0;
+    if (count_only) {
+        HJ_TRY(do_probe(c, kWide, probe, nullptr, nullptr, 0, (uint64_t *)c->dcount, true, st));
+        HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        *m = (int64_t)cnt;
+        return HJ_OK;
+    }
+    int64_t cap = ns > 0 ? ns : 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        HJ_TRY(dbuf(c, 2, sizeof(int64_t) * (size_t)cap, d_or));
+        HJ_TRY(dbuf(c, 3, sizeof(int64_t) * (size_t)cap, d_os));
+        HJ_TRY(do_probe(c, kWide, probe, *d_or, *d_os, cap, (uint64_t *)c->dcount, false, st));
+        HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        if ((int64_t)cnt <= cap) break;
+        cap = (int64_t)cnt;
+    }
+    *m = (int64_t)cnt;
+    return HJ_OK;
+}
+
+// Device column -> strided host memref.
+template <class T>
+int download(T *aligned, int64_t off, int64_t size, int64_t stride, const void *src, hipStream_t st) {
+    if (size <= 0) return HJ_OK;
+    if (!aligned) HJ_FAIL(HJ_ERR_ARG, "null output memref");
+    T *base = aligned + off;
+    if (stride == 1) {
+        HJ_HIP(hipMemcpyAsync(base, src, sizeof(T) * (size_t)size, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        return HJ_OK;
+    }
+    std::vector<T> tmp((size_t)size);
+    HJ_HIP(hipMemcpyAsync(tmp.data(), src, sizeof(T) * (size_t)size, hipMemcpyDeviceToHost, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    for (int64_t i = 0; i < size; ++i) base[i * stride] = tmp[(size_t)i];
+    return HJ_OK;
+}
+
+// Interleave two device columns into a malloc'ed memref<?x2xT> descriptor.
+template <class T, class D>
+int fill_result(D *res, const void *d_r, const void *d_s, int64_t m, hipStream_t st) {
+    std::memset(res, 0, sizeof(D));
+    T *buf = (T *)std::malloc(sizeof(T) * 2 * (size_t)(m > 0 ? m : 1));
+    if (!buf) HJ_FAIL(HJ_ERR_NOMEM, "malloc result");
+    if (m > 0) {
+        std::vector<T> a((size_t)m), b((size_t)m);
+        HJ_HIP(hipMemcpyAsync(a.data(), d_r, sizeof(T) * (size_t)m, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipMemcpyAsync(b.data(), d_s, sizeof(T) * (size_t)m, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        for (int64_t i = 0; i < m; ++i) {
+            buf[2 * i] = a[(size_t)i];
+            buf[2 * i + 1] = b[(size_t)i];
+        }
+    }
+    res->allocated = buf;
+    res->aligned = buf;
+    res->offset = 0;
+    res->sizes[0] = m;
+    res->sizes[1] = 2;
+    res->strides[0] = 2;
+    res->strides[1] = 1;
+    return HJ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hj_abi_version(void) { return HJ_ABI_VERSION; }
+const char *hj_last_error(void) { return g_err.c_str(); }
+
+hj_ctx *hj_ctx_create(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        fail(HJ_ERR_HIP, __FILE__, __LINE__, "no HIP device visible");
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        fail(HJ_ERR_ARG, __FILE__, __LINE__, "device index out of range");
+        return nullptr;
+    }
+    hj_ctx *c = new hj_ctx();
+    c->device = device;
+    if (set_device(c) != HJ_OK || ensure_meta(c, 64) != HJ_OK) {
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void hj_ctx_destroy(hj_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->table) (void)hipFree(c->table);
+    if (c->side) (void)hipFree(c->side);
+    if (c->meta) (void)hipFree(c->meta);
+    if (c->dcount) (void)hipFree(c->dcount);
+    for (int i = 0; i < 6; ++i)
+        if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
+    if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
+    if (c->ev_ready)
+        for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
+    {
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        for (auto it = g_default.begin(); it != g_default.end(); ++it)
+            if (it->second == c) {
+                g_default.erase(it);
+                break;
+            }
+    }
+    delete c;
+}
+
+int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (max_build_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
+    HJ_TRY(set_device(c));
+    return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
+}
+
+int64_t hj_ctx_table_capacity(const hj_ctx *c) { return (c && c->layout >= 0) ? (int64_t)(1ll << c->bits) : 0; }
+
+int hj_ctx_build_has_duplicates(hj_ctx *c) {
+    if (!c || c->layout < 0) HJ_FAIL(HJ_ERR_STATE, "no table built");
+    HJ_TRY(set_device(c));
+    unsigned long long v = 0;
+    HJ_HIP(hipDeviceSynchronize());
+    HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
+    return v ? 1 : 0;
+}
+
+int hj_ctx_set_timing(hj_ctx *c, int enable) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    HJ_TRY(set_device(c));
+    if (enable && !c->ev_ready) {
+        for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->ev[i]));
+        c->ev_ready = true;
+    }
+    c->timing = enable != 0;
+    return HJ_OK;
+}
+
+int hj_ctx_last_timing(hj_ctx *c, float ms[4]) {
+    if (!c || !ms) HJ_FAIL(HJ_ERR_ARG, "null argument");
+    for (int i = 0; i < 4; ++i) ms[i] = -1.0f;
+    if (!c->ev_ready) return HJ_OK;
+    HJ_TRY(set_device(c));
+    const int pairs[4][2] = {{kEvInit0, kEvInit1}, {kEvInit1, kEvBuild1}, {kEvProbe0, kEvProbe1}, {kEvPart0, kEvPart1}};
+    for (int i = 0; i < 4; ++i) {
+        if (!c->rec[i]) continue;
+        HJ_HIP(hipEventSynchronize(c->ev[pairs[i][1]]));
+        HJ_HIP(hipEventElapsedTime(&ms[i], c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
+    }
+    return HJ_OK;
+}
+
+// ------------------------------------------------------------ device phases
+int hj_dev_build_i64(hj_ctx *c, const int64_t *rkey, const int64_t *rpay, int64_t n, void *stream) {
+    return do_build(c, kWide, src_cols64(rkey, rpay, n), (hipStream_t)stream);
+}
+int hj_dev_count_i64(hj_ctx *c, const int64_t *skey, int64_t n, uint64_t *d_count, void *stream) {
+    hj::SrcDev s = src_cols64(skey, skey, n);   // payload unused when counting
+    return do_probe(c, kWide, s, nullptr, nullptr, 0, d_count, true, (hipStream_t)stream);
+}
+int hj_dev_probe_i64(hj_ctx *c, const int64_t *skey, const int64_t *spay, int64_t n, int64_t *out_r,
+                     int64_t *out_s, int64_t out_cap, uint64_t *d_count, void *stream) {
+    if (n > 0 && !spay) HJ_FAIL(HJ_ERR_ARG, "null probe payload");
+    return do_probe(c, kWide, src_cols64(skey, spay, n), out_r, out_s, out_cap, d_count, false,
+                    (hipStream_t)stream);
+}
+int hj_dev_build_tuples_i64(hj_ctx *c, const int64_t *tuples, int64_t n, void *stream) {
+    return do_build(c, kWide, src_packed(tuples, n), (hipStream_t)stream);
+}
+int hj_dev_probe_tuples_i64(hj_ctx *c, const int64_t *tuples, int64_t n, int64_t *out_r, int64_t *out_s,
+                            int64_t out_cap, uint64_t *d_count, void *stream) {
+    return do_probe(c, kWide, src_packed(tuples, n), out_r, out_s, out_cap, d_count, false, (hipStream_t)stream);
+}
+int hj_dev_build_i32(hj_ctx *c, const int32_t *rkey, int64_t n, int64_t row_base, void *stream) {
+    if (row_base < 0 || row_base + n > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids out of range");
+    return do_build(c, kNarrow, src_col32(rkey, n, row_base), (hipStream_t)stream);
+}
+int hj_dev_count_i32(hj_ctx *c, const int32_t *skey, int64_t n, uint64_t *d_count, void *stream) {
+    return do_probe(c, kNarrow, src_col32(skey, n, 0), nullptr, nullptr, 0, d_count, true, (hipStream_t)stream);
+}
+int hj_dev_probe_i32(hj_ctx *c, const int32_t *skey, int64_t n, int64_t row_base, int32_t *out_r, int32_t *out_s,
+                     int64_t out_cap, uint64_t *d_count, void *stream) {
+    if (row_base < 0 || row_base + n > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids out of range");
+    return do_probe(c, kNarrow, src_col32(skey, n, row_base), out_r, out_s, out_cap, d_count, false,
+                    (hipStream_t)stream);
+}
+
+int hj_dev_partition_i64(hj_ctx *c, const int64_t *key, const int64_t *pay, int64_t n, int nparts,
+                         int64_t *out_tuples, uint64_t *d_counts, void *stream) {
+    if (n > 0 && !pay) HJ_FAIL(HJ_ERR_ARG, "null payload");
+    return do_partition(c, src_cols64(key, pay, n), nparts, out_tuples, d_counts, (hipStream_t)stream);
+}
+int hj_dev_partition_tuples_i64(hj_ctx *c, const int64_t *tuples, int64_t n, int nparts, int64_t *out_tuples,
+                                uint64_t *d_counts, void *stream) {
+    return do_partition(c, src_packed(tuples, n), nparts, out_tuples, d_counts, (hipStream_t)stream);
+}
+
+int hj_partition_of(int64_t key, int nparts) {
+    if (nparts < 1) return -1;
+    unsigned long long k = (unsigned long long)key;
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return (int)(((k >> 32) * (unsigned long long)(unsigned)nparts) >> 32);
+}
+
+int hj_dev_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_threshold, int64_t r0, int64_t nr, int64_t *rkey,
+                        int64_t *rpay, int64_t s0, int64_t ns, int64_t *skey, int64_t *spay, void *stream) {
+    if (NR <= 0 || nr < 0 || ns < 0) HJ_FAIL(HJ_ERR_ARG, "bad generator sizes");
+    HJ_HIP(hj::launch_gen_pkfk(seed, NR, hit_threshold, r0, nr, (long long *)rkey, (long long *)rpay, s0, ns,
+                               (long long *)skey, (long long *)spay, (hipStream_t)stream));
+    return HJ_OK;
+}
+int hj_dev_gen_uniform_i64(uint64_t seed, uint64_t stream_id, int64_t lo, int64_t hi, int64_t i0, int64_t n,
+                           int64_t *key, int64_t *pay, void *stream) {
+    if (hi < lo || n < 0) HJ_FAIL(HJ_ERR_ARG, "bad generator range");
+    HJ_HIP(hj::launch_gen_uniform_i64(seed, stream_id, lo, hi, i0, n, (long long *)key, (long long *)pay,
+                                      (hipStream_t)stream));
+    return HJ_OK;
+}
+int hj_dev_gen_uniform_i32(uint64_t seed, uint64_t stream_id, int32_t lo, int32_t hi, int64_t i0, int64_t n,
+                           int32_t *key, void *stream) {
+    if (hi < lo || n < 0) HJ_FAIL(HJ_ERR_ARG, "bad generator range");
+    HJ_HIP(hj::launch_gen_uniform_i32(seed, stream_id, lo, hi, i0, n, key, (hipStream_t)stream));
+    return HJ_OK;
+}
+
+// ------------------------------------------------------- host memref ABI
+int64_t hj_count_i32(int32_t *, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride, int32_t *,
+                     int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride) {
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0;
+    void *a, *b;
+    int rc = host_join_i32(c, r_align, r_off, r_size, r_stride, s_align, s_off, s_size, s_stride, true, &m, &a, &b);
+    return rc == HJ_OK ? m : rc;
+}
+
+int32_t hj_probe_i32(int32_t *, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride, int32_t *,
+                     int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride, int32_t *,
+                     int32_t *or_align, int64_t or_off, int64_t or_size, int64_t or_stride, int32_t *,
+                     int32_t *os_align, int64_t os_off, int64_t os_size, int64_t os_stride) {
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0;
+    void *d_or = nullptr, *d_os = nullptr;
+    HJ_TRY(host_join_i32(c, r_align, r_off, r_size, r_stride, s_align, s_off, s_size, s_stride, false, &m, &d_or,
+                         &d_os));
+    if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
+    HJ_TRY(download<int32_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
+    HJ_TRY(download<int32_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));
+    return HJ_OK;
+}
+
+int64_t hj_count_i64(int64_t *, int64_t *rk, int64_t rk_off, int64_t rk_size, int64_t rk_stride, int64_t *,
+                     int64_t *rp, int64_t rp_off, int64_t rp_size, int64_t rp_stride, int64_t *, int64_t *sk,
+                     int64_t sk_off, int64_t sk_size, int64_t sk_stride, int64_t *, int64_t *sp, int64_t sp_off,
+                     int64_t sp_size, int64_t sp_stride) {
+    if (rk_size != rp_size || sk_size != sp_size) HJ_FAIL(HJ_ERR_ARG, "key/payload sizes differ");
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0;
+    void *a, *b;
+    int rc = host_join_i64(c, rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size, sk, sk_off, sk_stride, sp,
+                           sp_off, sp_stride, sk_size, true, &m, &a, &b);
+    return rc == HJ_OK ? m : rc;
+}
+
+int32_t hj_probe_i64(int64_t *, int64_t *rk, int64_t rk_off, int64_t rk_size, int64_t rk_stride, int64_t *,
+                     int64_t *rp, int64_t rp_off, int64_t rp_size, int64_t rp_stride, int64_t *, int64_t *sk,
+                     int64_t sk_off, int64_t sk_size, int64_t sk_stride, int64_t *, int64_t *sp, int64_t sp_off,
+                     int64_t sp_size, int64_t sp_stride, int64_t *, int64_t *or_align, int64_t or_off,
+                     int64_t or_size, int64_t or_stride, int64_t *, int64_t *os_align, int64_t os_off,
+                     int64_t os_size, int64_t os_stride) {
+    if (rk_size != rp_size || sk_size != sp_size) HJ_FAIL(HJ_ERR_ARG, "key/payload sizes differ");
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0;
+    void *d_or = nullptr, *d_os = nullptr;
+    HJ_TRY(host_join_i64(c, rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size, sk, sk_off, sk_stride, sp,
+                         sp_off, sp_stride, sk_size, false, &m, &d_or, &d_os));
+    if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
+    HJ_TRY(download<int64_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
+    HJ_TRY(download<int64_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));
+    return HJ_OK;
+}
+
+// ------------------------------------------------------ MLIR C-interface
+void _mlir_ciface_hj_join_i32(hj_memref2_i32 *res, hj_memref1_i32 *r, hj_memref1_i32 *s) {
+    if (!res) return;
+    std::memset(res, 0, sizeof(*res));
+    if (!r || !s) {
+        fail(HJ_ERR_ARG, __FILE__, __LINE__, "null memref descriptor");
+        return;
+    }
+    hj_ctx *c = default_ctx();
+    if (!c) return;
+    int64_t m = 0;
+    void *d_or = nullptr, *d_os = nullptr;
+    if (host_join_i32(c, r->aligned, r->offset, r->sizes[0], r->strides[0], s->aligned, s->offset, s->sizes[0],
+                      s->strides[0], false, &m, &d_or, &d_os) != HJ_OK)
+        return;
+    fill_result<int32_t>(res, d_or, d_os, m, c->host_stream);
+}
+
+void _mlir_ciface_hj_join_i64(hj_memref2_i64 *res, hj_memref1_i64 *r, hj_memref1_i64 *s) {
+    if (!res) return;
+    std::memset(res, 0, sizeof(*res));
+    if (!r || !s) {
+        fail(HJ_ERR_ARG, __FILE__, __LINE__, "null memref descriptor");
+        return;
+    }
+    hj_ctx *c = default_ctx();
+    if (!c) return;
+    int64_t m = 0;
+    void *d_or = nullptr, *d_os = nullptr;
+    if (host_join_i64(c, r->aligned, r->offset, r->strides[0], nullptr, 0, 1, r->sizes[0], s->aligned, s->offset,
+                      s->strides[0], nullptr, 0, 1, s->sizes[0], false, &m, &d_or, &d_os) != HJ_OK)
+        return;
+    fill_result<int64_t>(res, d_or, d_os, m, c->host_stream);
+}
+
+void _mlir_ciface_hj_join_kp_i64(hj_memref2_i64 *res, hj_memref1_i64 *rk, hj_memref1_i64 *rp, hj_memref1_i64 *sk,
+                                 hj_memref1_i64 *sp) {
+    if (!res) return;
+    std::memset(res, 0, sizeof(*res));
+    if (!rk || !rp || !sk || !sp || rk->sizes[0] != rp->sizes[0] || sk->sizes[0] != sp->sizes[0]) {
+        fail(HJ_ERR_ARG, __FILE__, __LINE__, "bad key/payload memrefs");
+        return;
+    }
+    hj_ctx *c = default_ctx();
+    if (!c) return;
+    int64_t m = 0;
+    void *d_or = nullptr, *d_os = nullptr;
+    if (host_join_i64(c, rk->aligned, rk->offset, rk->strides[0], rp->aligned, rp->offset, rp->strides[0],
+                      rk->sizes[0], sk->aligned, sk->offset, sk->strides[0], sp->aligned, sp->offset,
+                      sp->strides[0], sk->sizes[0], false, &m, &d_or, &d_os) != HJ_OK)
+        return;
+    fill_result<int64_t>(res, d_or, d_os, m, c->host_stream);
+}
+
+void hj_free_result(void *allocated) { std::free(allocated); }
+
+}  // extern "C"

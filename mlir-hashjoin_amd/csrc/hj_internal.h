@@ -1,0 +1,84 @@
+// hj_internal.h -- device data layout and kernel launchers of the MI355X
+// hash join.  Not part of the public ABI (that is include/hj.h).
+//
+// Hash table = open addressing with linear probing (north_star), replacing the
+// reference's bucket-chained heads + SoA linked list (join_v1.mlir:25-39,
+// :213-249).  Two slot layouts:
+//
+//   wide   : 16-B slot {u64 key, u64 payload}; EMPTY key = INT64_MIN.
+//            R rows whose key IS INT64_MIN go to a side list (payload only)
+//            and are matched by a side loop whose cost is proportional to
+//            the output it produces.
+//   narrow : 8-B slot (u32 key << 32 | u32 row id), the reference's i32 key /
+//            i32 row-id types (join_v1.mlir:546-549, :604-605).  Row ids are
+//            < 2^31, so the all-ones word can never be a real slot: EMPTY.
+//
+// Both: power-of-two capacity >= 2 * |R| (load factor <= 0.5), slot index =
+// top bits of a Fibonacci multiplicative hash, one 64-bit atomicCAS claims a
+// slot; duplicate build keys each take their own slot (the reference visits
+// every chain node, join_v2.mlir:363-384, so duplicates must all match).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hj {
+
+constexpr unsigned long long kEmptyKey64 = 0x8000000000000000ull;
+constexpr unsigned long long kEmptySlot32 = ~0ull;
+
+struct alignas(16) Slot64 {
+    unsigned long long key;
+    unsigned long long pay;
+};
+
+// Device-side table descriptor, passed by value to kernels.
+struct TableDev {
+    void *slots;                     // Slot64[cap] or u64[cap]
+    unsigned long long mask;         // cap - 1
+    int shift;                       // 64 - log2(cap)
+    unsigned long long *side;        // wide: payloads of INT64_MIN-key rows
+    unsigned long long *meta;        // [0] side count, [1] dup-seen flag, [2..] scratch counters
+};
+
+enum Layout : int { kWide = 0, kNarrow = 1 };
+
+// Source forms of a relation on the device.
+enum SrcForm : int { kCols64 = 0, kPacked64 = 1, kCol32 = 2 };
+
+struct SrcDev {
+    const void *key;    // int64 column, packed {key,pay} tuples, or int32 column
+    const void *pay;    // int64 column (kCols64 only)
+    long long n;
+    long long row_base; // kCol32: row id = row_base + row
+    int form;
+};
+
+struct OutDev {
+    void *r;            // int64 or int32 column (R payload / row id)
+    void *s;            // int64 or int32 column (S payload / row id)
+    long long cap;      // rows the caller allocated
+    unsigned long long *counter;  // device u64: total match count (all rows, even past cap)
+};
+
+// launchers (hipError_t of the launch; all asynchronous on `st`)
+hipError_t launch_init(const TableDev &t, int layout, unsigned long long cap, hipStream_t st);
+hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStream_t st);
+hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
+                        bool count_only, hipStream_t st);
+
+hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
+                            unsigned long long *counts, unsigned long long *cursors,
+                            hipStream_t st);
+
+hipError_t launch_gen_pkfk(unsigned long long seed, long long NR, unsigned long long hit_thr,
+                           long long r0, long long nr, long long *rkey, long long *rpay,
+                           long long s0, long long ns, long long *skey, long long *spay,
+                           hipStream_t st);
+hipError_t launch_gen_uniform_i64(unsigned long long seed, unsigned long long stream_id,
+                                  long long lo, long long hi, long long i0, long long n,
+                                  long long *key, long long *pay, hipStream_t st);
+hipError_t launch_gen_uniform_i32(unsigned long long seed, unsigned long long stream_id,
+                                  int lo, int hi, long long i0, long long n, int *key,
+                                  hipStream_t st);
+
+}  // namespace hj

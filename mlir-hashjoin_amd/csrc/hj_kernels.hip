@@ -1,0 +1,506 @@
+// hj_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the hash join.
+//
+// Reference kernels replaced (kernel inventory):
+//   initializeHT  join_v1.mlir:180-202  -> k_init    (slot fill, 16 B/lane)
+//   build         join_v1.mlir:213-277  -> k_build   (linear probing, 64-bit CAS)
+//   count         join_v1.mlir:288-425  -> k_probe<WRITE=false>
+//   probe v1/v2   join_v1.mlir:436-521, join_v2.mlir:450-604
+//                                       -> k_probe<WRITE=true>: LDS-staged
+//                                          output block, one global cursor
+//                                          add per block, coalesced flush
+// plus the radix partition used by the multi-GPU exchange and the
+// counter-based generators of the benchmark inputs.
+//
+// Wave64 throughout: 256-thread blocks (4 waves), all per-lane work
+// independent, no warp-32 idioms.  Integer/byte work: no MFMA.
+#include "hj_internal.h"
+#include "hj_gen.h"
+
+namespace hj {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kBuildItems = 4;   // rows per thread in build (CAS ILP)
+constexpr int kProbeItems = 4;   // rows per thread in probe (tile = 1024 rows)
+constexpr int kPartItems = 8;    // rows per thread in partition
+
+__device__ __forceinline__ unsigned long long slot_of(unsigned long long k, int shift) {
+    return (k * 0x9E3779B97F4A7C15ull) >> shift;   // Fibonacci hashing, top bits
+}
+
+// ------------------------------------------------------------------ sources
+struct Tuple {
+    unsigned long long k, p;
+};
+
+template <int FORM>
+__device__ __forceinline__ Tuple load_src(const SrcDev &s, long long row);
+
+template <>
+__device__ __forceinline__ Tuple load_src<kCols64>(const SrcDev &s, long long row) {
+    return {((const unsigned long long *)s.key)[row], ((const unsigned long long *)s.pay)[row]};
+}
+template <>
+__device__ __forceinline__ Tuple load_src<kPacked64>(const SrcDev &s, long long row) {
+    const ulonglong2 v = ((const ulonglong2 *)s.key)[row];
+    return {v.x, v.y};
+}
+template <>
+__device__ __forceinline__ Tuple load_src<kCol32>(const SrcDev &s, long long row) {
+    return {(unsigned long long)(unsigned)((const int *)s.key)[row],
+            (unsigned long long)(s.row_base + row)};
+}
+
+// ------------------------------------------------------------------ layouts
+template <int L>
+struct Lay;
+
+template <>
+struct Lay<kWide> {
+    using slot_t = Slot64;
+    using out_t = long long;
+    static constexpr unsigned long long kEmptyWord = kEmptyKey64;
+    static __device__ __forceinline__ unsigned long long *word(slot_t *sl, unsigned long long h) { return &sl[h].key; }
+    static __device__ __forceinline__ unsigned long long cas_val(unsigned long long k, unsigned long long) { return k; }
+    static __device__ __forceinline__ unsigned long long word_key(unsigned long long w) { return w; }
+    static __device__ __forceinline__ void after_claim(slot_t *sl, unsigned long long h, unsigned long long p) { sl[h].pay = p; }
+    static __device__ __forceinline__ bool empty(const slot_t &s) { return s.key == kEmptyKey64; }
+    static __device__ __forceinline__ unsigned long long key(const slot_t &s) { return s.key; }
+    static __device__ __forceinline__ unsigned long long pay(const slot_t &s) { return s.pay; }
+    static __device__ __forceinline__ bool null_key(unsigned long long k) { return k == kEmptyKey64; }
+};
+
+template <>
+struct Lay<kNarrow> {
+    using slot_t = unsigned long long;
+    using out_t = int;
+    static constexpr unsigned long long kEmptyWord = kEmptySlot32;
+    static __device__ __forceinline__ unsigned long long *word(slot_t *sl, unsigned long long h) { return &sl[h]; }
+    static __device__ __forceinline__ unsigned long long cas_val(unsigned long long k, unsigned long long p) { return (k << 32) | (p & 0xffffffffull); }
+    static __device__ __forceinline__ unsigned long long word_key(unsigned long long w) { return w >> 32; }
+    static __device__ __forceinline__ void after_claim(slot_t *, unsigned long long, unsigned long long) {}
+    static __device__ __forceinline__ bool empty(const slot_t &s) { return s == kEmptySlot32; }
+    static __device__ __forceinline__ unsigned long long key(const slot_t &s) { return s >> 32; }
+    static __device__ __forceinline__ unsigned long long pay(const slot_t &s) { return s & 0xffffffffull; }
+    static __device__ __forceinline__ bool null_key(unsigned long long) { return false; }
+};
+
+template <int N, typename T>
+__device__ __forceinline__ T pick(const T (&a)[N], int i) {   // static-index select: no scratch
+    T r = a[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j) r = (i == j) ? a[j] : r;
+    return r;
+}
+
+// ------------------------------------------------------------------ init
+// initializeHT (join_v2.mlir:203-225) sets heads[:] = -1; here every slot is
+// set EMPTY with 16-B stores, and the side count / dup flag are reset.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_init(TableDev t, unsigned long long n16) {
+    const ulonglong2 v = (L == kWide) ? make_ulonglong2(kEmptyKey64, 0ull)
+                                      : make_ulonglong2(kEmptySlot32, kEmptySlot32);
+    ulonglong2 *p = (ulonglong2 *)t.slots;
+    const unsigned long long base = (unsigned long long)blockIdx.x * (kBlock * 4) + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const unsigned long long j = base + (unsigned long long)i * kBlock;
+        if (j < n16) p[j] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 2) t.meta[threadIdx.x] = 0ull;
+}
+
+// ------------------------------------------------------------------ build
+// build + @insertNodeInHashTable (join_v2.mlir:236-300): the reference takes
+// a node with atomicAdd(freeIndex) -- one address hit by every thread -- and
+// prepends it with atomicExch on the bucket head.  Here each row claims its
+// own slot with one 64-bit CAS at its hash position (linear probing on
+// failure).  The first CAS of all kBuildItems rows is issued before any
+// result is consumed, so each lane has that many atomics in flight.
+// A failed CAS that returns the row's own key proves the build side has a
+// duplicate key (both rows walk the same probe sequence, so the later one
+// must fail on the earlier one's slot); that sets meta[1], and probes then
+// keep walking past matches.  Without duplicates a probe stops at its match.
+template <int L, int FORM>
+__global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
+    using LY = Lay<L>;
+    using slot_t = typename LY::slot_t;
+    slot_t *sl = (slot_t *)t.slots;
+    const long long base = (long long)blockIdx.x * (kBlock * kBuildItems) + threadIdx.x;
+    unsigned long long k[kBuildItems], p[kBuildItems], h[kBuildItems], o[kBuildItems];
+    bool v[kBuildItems];
+#pragma unroll
+    for (int i = 0; i < kBuildItems; ++i) {
+        const long long row = base + (long long)i * kBlock;
+        v[i] = row < src.n;
+        Tuple tp = v[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
+        k[i] = tp.k;
+        p[i] = tp.p;
+    }
+#pragma unroll
+    for (int i = 0; i < kBuildItems; ++i) {
+        if (v[i] && LY::null_key(k[i])) {   // wide only: INT64_MIN keys -> side list
+            const unsigned long long idx = atomicAdd(&t.meta[0], 1ull);
+            t.side[idx] = p[i];
+            v[i] = false;
+        }
+        h[i] = slot_of(k[i], t.shift);
+        o[i] = v[i] ? atomicCAS(LY::word(sl, h[i]), LY::kEmptyWord, LY::cas_val(k[i], p[i]))
+                    : LY::kEmptyWord;
+    }
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < kBuildItems; ++i) {
+        if (!v[i]) continue;
+        unsigned long long hh = h[i], old = o[i];
+        while (old != LY::kEmptyWord) {
+            dup |= (LY::word_key(old) == k[i]);
+            hh = (hh + 1) & t.mask;
+            old = atomicCAS(LY::word(sl, hh), LY::kEmptyWord, LY::cas_val(k[i], p[i]));
+        }
+        LY::after_claim(sl, hh, p[i]);
+    }
+    if (dup) __hip_atomic_store(&t.meta[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ probe
+// count (join_v2.mlir:311-439) and probe (join_v1.mlir:436-521,
+// join_v2.mlir:450-604) in one kernel family.
+//
+// Each thread owns kProbeItems rows of a 1024-row tile (coalesced loads,
+// statically indexed registers).  The probe of a lane is one flattened loop:
+// every iteration issues exactly one slot load; when the current row is
+// resolved (EMPTY reached, or matched with a duplicate-free build side) the
+// lane moves to its next row, so the wave runs max(sum of probe lengths)
+// iterations instead of sum(max) -- divergence across rows is absorbed.
+//
+// Output (WRITE): matches are staged in LDS (the v2 idea, join_v2.mlir:
+// 525-538) through a wave-aggregated LDS cursor; the tile then reserves its
+// range with ONE global 64-bit atomic add and flushes coalesced (8 B/lane per
+// column).  Tiles producing more than 1024 matches spill the excess straight
+// to global through the same cursor (the v2 overflow path, :539-549).  The
+// cursor counts every match, so a caller whose capacity was too small still
+// learns the exact M (rows past cap are dropped).
+template <int L, int FORM, bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out) {
+    using LY = Lay<L>;
+    using slot_t = typename LY::slot_t;
+    using out_t = typename LY::out_t;
+    constexpr int kTile = kBlock * kProbeItems;
+    __shared__ out_t st_r[WRITE ? kTile : 1];
+    __shared__ out_t st_s[WRITE ? kTile : 1];
+    __shared__ unsigned st_n;
+    __shared__ unsigned long long st_base;
+    __shared__ unsigned long long wsum[kBlock / 64];
+
+    const slot_t *sl = (const slot_t *)t.slots;
+    if (threadIdx.x == 0) st_n = 0u;
+    const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
+
+    const long long base = (long long)blockIdx.x * kTile + threadIdx.x;
+    unsigned long long K[kProbeItems], P[kProbeItems];
+    bool V[kProbeItems];
+#pragma unroll
+    for (int i = 0; i < kProbeItems; ++i) {
+        const long long row = base + (long long)i * kBlock;
+        V[i] = row < src.n;
+        Tuple tp = V[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
+        K[i] = tp.k;
+        P[i] = tp.p;
+    }
+    __syncthreads();   // st_n visible
+
+    unsigned long long cnt = 0;
+    auto emit = [&](unsigned long long rv, unsigned long long sv) {
+        if constexpr (!WRITE) {
+            ++cnt;
+        } else {
+            const unsigned idx = atomicAdd(&st_n, 1u);
+            if (idx < (unsigned)kTile) {
+                st_r[idx] = (out_t)rv;
+                st_s[idx] = (out_t)sv;
+            } else {
+                const unsigned long long g = atomicAdd(out.counter, 1ull);
+                if (g < (unsigned long long)out.cap) {
+                    ((out_t *)out.r)[g] = (out_t)rv;
+                    ((out_t *)out.s)[g] = (out_t)sv;
+                }
+            }
+        }
+    };
+
+    int it = -1;
+    bool have = false;
+    unsigned long long k = 0, p = 0, hh = 0;
+    while (true) {
+        while (!have) {
+            if (++it >= kProbeItems) break;
+            if (!pick(V, it)) continue;
+            k = pick(K, it);
+            p = pick(P, it);
+            if (LY::null_key(k)) {   // wide: INT64_MIN probe key matches every side row
+                const unsigned long long ns = t.meta[0];
+                for (unsigned long long j = 0; j < ns; ++j) emit(t.side[j], p);
+                continue;
+            }
+            hh = slot_of(k, t.shift);
+            have = true;
+        }
+        if (!have) break;
+        const slot_t s = sl[hh];
+        if (LY::empty(s)) {
+            have = false;
+        } else {
+            if (LY::key(s) == k) {
+                emit(LY::pay(s), p);
+                if (unique) have = false;
+            }
+            hh = (hh + 1) & t.mask;
+        }
+    }
+
+    if constexpr (WRITE) {
+        __syncthreads();
+        const unsigned nb = st_n;
+        const unsigned nl = nb < (unsigned)kTile ? nb : (unsigned)kTile;
+        if (threadIdx.x == 0) st_base = nl ? atomicAdd(out.counter, (unsigned long long)nl) : 0ull;
+        __syncthreads();
+        const unsigned long long gb = st_base;
+        out_t *orr = (out_t *)out.r;
+        out_t *oss = (out_t *)out.s;
+        for (unsigned j = threadIdx.x; j < nl; j += kBlock) {
+            const unsigned long long g = gb + j;
+            if (g < (unsigned long long)out.cap) {
+                orr[g] = st_r[j];
+                oss[g] = st_s[j];
+            }
+        }
+    } else {
+        // block total: wave reduction (64 lanes) then one add per block
+        unsigned long long c = cnt;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tot = 0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) tot += wsum[w];
+            if (tot) atomicAdd(out.counter, tot);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ partition
+// Radix partition by a hash independent of the slot hash (fmix64 top word,
+// multiply-shift onto [0, P)), so a partition's keys still spread over its
+// local table.  Used to route R and S rows to their owning GPU.
+__device__ __forceinline__ unsigned part_of(unsigned long long k, unsigned P) {
+    return (unsigned)(((fmix64(k) >> 32) * (unsigned long long)P) >> 32);
+}
+
+template <int FORM>
+__global__ __launch_bounds__(kBlock) void k_part_hist(SrcDev src, unsigned P, unsigned long long *counts) {
+    extern __shared__ unsigned lds_hist[];
+    for (unsigned i = threadIdx.x; i < P; i += kBlock) lds_hist[i] = 0u;
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * (kBlock * kPartItems) + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+        const long long row = base + (long long)i * kBlock;
+        if (row < src.n) atomicAdd(&lds_hist[part_of(load_src<FORM>(src, row).k, P)], 1u);
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < P; i += kBlock)
+        if (lds_hist[i]) atomicAdd(&counts[i], (unsigned long long)lds_hist[i]);
+}
+
+__global__ void k_part_offsets(const unsigned long long *counts, unsigned P, unsigned long long *cursors) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        unsigned long long acc = 0;
+        for (unsigned i = 0; i < P; ++i) {
+            cursors[i] = acc;
+            acc += counts[i];
+        }
+    }
+}
+
+template <int FORM>
+__global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P, ulonglong2 *out,
+                                                         unsigned long long *cursors) {
+    extern __shared__ unsigned lds[];   // [0,P) local counts -> ranks, [P,3P) u64 bases
+    unsigned *cnt = lds;
+    unsigned long long *bases = (unsigned long long *)(lds + ((P + 1) & ~1u));
+    for (unsigned i = threadIdx.x; i < P; i += kBlock) cnt[i] = 0u;
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * (kBlock * kPartItems) + threadIdx.x;
+    unsigned long long k[kPartItems], p[kPartItems];
+    unsigned pid[kPartItems];
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+        const long long row = base + (long long)i * kBlock;
+        if (row < src.n) {
+            Tuple tp = load_src<FORM>(src, row);
+            k[i] = tp.k;
+            p[i] = tp.p;
+            pid[i] = part_of(tp.k, P);
+            atomicAdd(&cnt[pid[i]], 1u);
+        } else {
+            pid[i] = ~0u;
+            k[i] = p[i] = 0ull;
+        }
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < P; i += kBlock) {
+        const unsigned c = cnt[i];
+        bases[i] = c ? atomicAdd(&cursors[i], (unsigned long long)c) : 0ull;
+        cnt[i] = 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPartItems; ++i) {
+        if (pid[i] == ~0u) continue;
+        const unsigned r = atomicAdd(&cnt[pid[i]], 1u);
+        out[bases[pid[i]] + r] = make_ulonglong2(k[i], p[i]);
+    }
+}
+
+// ------------------------------------------------------------------ datagen
+__global__ __launch_bounds__(kBlock) void k_gen_pkfk(unsigned long long seed, long long NR,
+                                                     unsigned long long hit_thr, long long r0, long long nr,
+                                                     long long *rkey, long long *rpay, long long s0, long long ns,
+                                                     long long *skey, long long *spay) {
+    const unsigned long long salt = pkfk_salt(seed);
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i < nr) {
+        const unsigned long long g = (unsigned long long)(r0 + i);
+        rkey[i] = pkfk_rkey(salt, g);
+        rpay[i] = (long long)g;
+    }
+    if (i < ns) {
+        const unsigned long long g = (unsigned long long)(s0 + i);
+        skey[i] = pkfk_skey(seed, salt, NR, hit_thr, g);
+        spay[i] = (long long)g;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_uniform_i64(unsigned long long seed, unsigned long long sid,
+                                                            long long lo, long long hi, long long i0, long long n,
+                                                            long long *key, long long *pay) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long range = (unsigned long long)(hi - lo) + 1ull;
+    const unsigned long long g = (unsigned long long)(i0 + i);
+    const unsigned long long r = rand64(seed, sid, g);
+    key[i] = lo + (long long)(range ? r % range : r);
+    if (pay) pay[i] = (long long)g;
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_uniform_i32(unsigned long long seed, unsigned long long sid,
+                                                            int lo, int hi, long long i0, long long n, int *key) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long range = (unsigned long long)((long long)hi - (long long)lo) + 1ull;
+    const unsigned long long r = rand64(seed, sid, (unsigned long long)(i0 + i));
+    key[i] = (int)((long long)lo + (long long)(r % range));
+}
+
+inline unsigned grid_for(long long n, int per_block) {
+    return (unsigned)((n + per_block - 1) / per_block);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_init(const TableDev &t, int layout, unsigned long long cap, hipStream_t st) {
+    const unsigned long long bytes = cap * (layout == kWide ? 16ull : 8ull);
+    const unsigned long long n16 = bytes / 16ull;
+    const unsigned g = grid_for((long long)n16, kBlock * 4);
+    if (layout == kWide) hipLaunchKernelGGL(k_init<kWide>, dim3(g), dim3(kBlock), 0, st, t, n16);
+    else hipLaunchKernelGGL(k_init<kNarrow>, dim3(g), dim3(kBlock), 0, st, t, n16);
+    return hipGetLastError();
+}
+
+hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStream_t st) {
+    if (src.n <= 0) return hipSuccess;
+    const unsigned g = grid_for(src.n, kBlock * kBuildItems);
+    if (layout == kWide) {
+        if (src.form == kCols64) hipLaunchKernelGGL((k_build<kWide, kCols64>), dim3(g), dim3(kBlock), 0, st, t, src);
+        else if (src.form == kPacked64) hipLaunchKernelGGL((k_build<kWide, kPacked64>), dim3(g), dim3(kBlock), 0, st, t, src);
+        else return hipErrorInvalidValue;
+    } else {
+        if (src.form == kCol32) hipLaunchKernelGGL((k_build<kNarrow, kCol32>), dim3(g), dim3(kBlock), 0, st, t, src);
+        else return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
+                        bool count_only, hipStream_t st) {
+    if (src.n <= 0) return hipSuccess;
+    const unsigned g = grid_for(src.n, kBlock * kProbeItems);
+#define HJ_PROBE(L, F)                                                                             \
+    do {                                                                                           \
+        if (count_only) hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out); \
+        else hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out); \
+    } while (0)
+    if (layout == kWide) {
+        if (src.form == kCols64) HJ_PROBE(kWide, kCols64);
+        else if (src.form == kPacked64) HJ_PROBE(kWide, kPacked64);
+        else return hipErrorInvalidValue;
+    } else {
+        if (src.form == kCol32) HJ_PROBE(kNarrow, kCol32);
+        else return hipErrorInvalidValue;
+    }
+#undef HJ_PROBE
+    return hipGetLastError();
+}
+
+hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
+                            unsigned long long *counts, unsigned long long *cursors, hipStream_t st) {
+    const unsigned P = (unsigned)nparts;
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * P, st);
+    if (e != hipSuccess) return e;
+    if (src.n > 0) {
+        const unsigned g = grid_for(src.n, kBlock * kPartItems);
+        const size_t lds_h = sizeof(unsigned) * P;
+        const size_t lds_s = sizeof(unsigned) * ((P + 1) & ~1u) + sizeof(unsigned long long) * P;
+        if (src.form == kCols64) hipLaunchKernelGGL(k_part_hist<kCols64>, dim3(g), dim3(kBlock), lds_h, st, src, P, counts);
+        else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(g), dim3(kBlock), lds_h, st, src, P, counts);
+        else return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(64), 0, st, counts, P, cursors);
+        if (src.form == kCols64)
+            hipLaunchKernelGGL(k_part_scatter<kCols64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
+        else
+            hipLaunchKernelGGL(k_part_scatter<kPacked64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_pkfk(unsigned long long seed, long long NR, unsigned long long hit_thr,
+                           long long r0, long long nr, long long *rkey, long long *rpay,
+                           long long s0, long long ns, long long *skey, long long *spay, hipStream_t st) {
+    const long long n = nr > ns ? nr : ns;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_pkfk, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, seed, NR, hit_thr, r0, nr,
+                       rkey, rpay, s0, ns, skey, spay);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_uniform_i64(unsigned long long seed, unsigned long long sid, long long lo, long long hi,
+                                  long long i0, long long n, long long *key, long long *pay, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_uniform_i64, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, seed, sid, lo, hi, i0, n,
+                       key, pay);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_uniform_i32(unsigned long long seed, unsigned long long sid, int lo, int hi, long long i0,
+                                  long long n, int *key, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_uniform_i32, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, seed, sid, lo, hi, i0, n,
+                       key);
+    return hipGetLastError();
+}
+
+}  // namespace hj

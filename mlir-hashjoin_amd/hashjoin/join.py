@@ -1,0 +1,230 @@
+"""Host-side mirror of the reference's join program over device tensors.
+
+The reference's host functions (join_v2.mlir:25-199) map one-to-one:
+
+    @allocateHashTable     -> HashJoin.allocate_hash_table   (hj_ctx_reserve)
+    @initializeHashTable   -> HashJoin.build_table           (init + build
+    @buildTable               kernels, hj_dev_build_*)
+    @countRows             -> HashJoin.count_rows            (hj_dev_count_*)
+    @probeRelation         -> HashJoin.probe_relation        (hj_dev_probe_*)
+    @main's join sequence  -> HashJoin.join
+
+Tensors are PyTorch device tensors (plumbing only: allocation and the HIP
+stream); every computation runs in libhj.so's HIP kernels.  Key dtype picks
+the table layout: int64 keys -> 64-bit key/payload columns, int32 keys -> the
+reference's i32 keys with i32 row ids.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import check, lib
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device, stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return C.c_void_p(s.cuda_stream)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and (not t.is_cuda or not t.is_contiguous()):
+            raise ValueError("hash join inputs must be contiguous device tensors")
+
+
+class HashJoin:
+    """One device's hash-join context (table workspace + phase timing)."""
+
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("HashJoin needs a HIP device (no CPU fallback)")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self._ctx = lib.hj_ctx_create(self.device.index)
+        if not self._ctx:
+            raise RuntimeError("hj_ctx_create failed: " + lib.hj_last_error().decode())
+        self._count = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.key_bits = None
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib.hj_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- workspace
+    def allocate_hash_table(self, num_tuples, key_bits=64):
+        """@allocateHashTable (join_v2.mlir:25-39): size the workspace once."""
+        check(lib.hj_ctx_reserve(self._ctx, int(num_tuples), int(key_bits)), "hj_ctx_reserve")
+
+    @property
+    def capacity(self):
+        return int(lib.hj_ctx_table_capacity(self._ctx))
+
+    def has_duplicates(self):
+        r = lib.hj_ctx_build_has_duplicates(self._ctx)
+        if r < 0:
+            check(r, "hj_ctx_build_has_duplicates")
+        return bool(r)
+
+    def set_timing(self, enable=True):
+        check(lib.hj_ctx_set_timing(self._ctx, 1 if enable else 0), "hj_ctx_set_timing")
+
+    def last_timing(self):
+        """ms of the last (init, build, probe/count, partition) launches."""
+        a = (C.c_float * 4)()
+        check(lib.hj_ctx_last_timing(self._ctx, a), "hj_ctx_last_timing")
+        return dict(zip(("init", "build", "probe", "partition"), list(a)))
+
+    # -------------------------------------------------------------- phases
+    def build_table(self, rkey, rpay=None, row_base=0, stream=None):
+        """@initializeHashTable + @buildTable (join_v2.mlir:54-108)."""
+        _need_cuda(rkey, rpay)
+        st = _stream(self.device, stream)
+        if rkey.dtype == torch.int64:
+            if rpay is None or rpay.dtype != torch.int64 or rpay.numel() != rkey.numel():
+                raise ValueError("int64 build needs an int64 payload column of the same length")
+            check(lib.hj_dev_build_i64(self._ctx, _ptr(rkey), _ptr(rpay), rkey.numel(), st), "hj_dev_build_i64")
+            self.key_bits = 64
+        elif rkey.dtype == torch.int32:
+            if rpay is not None:
+                raise ValueError("i32 joins carry row ids, not payloads (reference types)")
+            check(lib.hj_dev_build_i32(self._ctx, _ptr(rkey), rkey.numel(), int(row_base), st), "hj_dev_build_i32")
+            self.key_bits = 32
+        else:
+            raise TypeError("keys must be int32 or int64")
+
+    def build_tuples(self, tuples, stream=None):
+        """Build from packed (n, 2) int64 {key, payload} rows (exchange format)."""
+        _need_cuda(tuples)
+        if tuples.dtype != torch.int64 or tuples.dim() != 2 or tuples.shape[1] != 2:
+            raise ValueError("tuples must be an (n, 2) int64 tensor")
+        check(lib.hj_dev_build_tuples_i64(self._ctx, _ptr(tuples), tuples.shape[0], _stream(self.device, stream)),
+              "hj_dev_build_tuples_i64")
+        self.key_bits = 64
+
+    def count_rows(self, skey, stream=None, sync=True):
+        """@countRows (join_v2.mlir:110-147): M, the result size."""
+        _need_cuda(skey)
+        st = _stream(self.device, stream)
+        if skey.dtype == torch.int64:
+            check(lib.hj_dev_count_i64(self._ctx, _ptr(skey), skey.numel(), _ptr(self._count), st), "hj_dev_count_i64")
+        else:
+            check(lib.hj_dev_count_i32(self._ctx, _ptr(skey), skey.numel(), _ptr(self._count), st), "hj_dev_count_i32")
+        return int(self._count.item()) if sync else self._count
+
+    def probe_relation(self, skey, spay=None, out_r=None, out_s=None, count=None, row_base=0, stream=None):
+        """@probeRelation (join_v2.mlir:149-199).  Writes min(M, cap) rows into
+        out_r / out_s; `count` (int64 device tensor) receives M.  Returns count."""
+        _need_cuda(skey, spay, out_r, out_s)
+        st = _stream(self.device, stream)
+        count = self._count if count is None else count
+        cap = 0 if out_r is None else out_r.numel()
+        if out_s is not None and out_s.numel() != cap:
+            raise ValueError("output columns differ in length")
+        if skey.dtype == torch.int64:
+            if spay is None or spay.dtype != torch.int64:
+                raise ValueError("int64 probe needs an int64 payload column")
+            check(lib.hj_dev_probe_i64(self._ctx, _ptr(skey), _ptr(spay), skey.numel(), _ptr(out_r), _ptr(out_s),
+                                       cap, _ptr(count), st), "hj_dev_probe_i64")
+        else:
+            check(lib.hj_dev_probe_i32(self._ctx, _ptr(skey), skey.numel(), int(row_base), _ptr(out_r), _ptr(out_s),
+                                       cap, _ptr(count), st), "hj_dev_probe_i32")
+        return count
+
+    def probe_tuples(self, tuples, out_r, out_s, count=None, stream=None):
+        _need_cuda(tuples, out_r, out_s)
+        count = self._count if count is None else count
+        check(lib.hj_dev_probe_tuples_i64(self._ctx, _ptr(tuples), tuples.shape[0], _ptr(out_r), _ptr(out_s),
+                                          out_r.numel(), _ptr(count), _stream(self.device, stream)),
+              "hj_dev_probe_tuples_i64")
+        return count
+
+    def partition(self, key, pay=None, nparts=2, out=None, counts=None, stream=None):
+        """Radix-route rows to nparts owners: packed (n, 2) tuples grouped by
+        owner + per-owner counts (int64 device tensor)."""
+        st = _stream(self.device, stream)
+        n = key.shape[0]
+        out = torch.empty((n, 2), dtype=torch.int64, device=self.device) if out is None else out
+        counts = torch.empty(nparts, dtype=torch.int64, device=self.device) if counts is None else counts
+        if pay is None:   # key is already packed tuples
+            _need_cuda(key, out, counts)
+            check(lib.hj_dev_partition_tuples_i64(self._ctx, _ptr(key), n, nparts, _ptr(out), _ptr(counts), st),
+                  "hj_dev_partition_tuples_i64")
+        else:
+            _need_cuda(key, pay, out, counts)
+            check(lib.hj_dev_partition_i64(self._ctx, _ptr(key), _ptr(pay), n, nparts, _ptr(out), _ptr(counts), st),
+                  "hj_dev_partition_i64")
+        return out, counts
+
+    # -------------------------------------------------------------- whole join
+    def join(self, rkey, rpay, skey, spay=None, capacity=None, stream=None):
+        """The @main join (join_v2.mlir:646-696) on device tensors: build, then
+        probe into an output sized optimistically (|S| rows, or `capacity`),
+        re-probing once at the exact M if that was too small."""
+        self.build_table(rkey, rpay, stream=stream)
+        dt = torch.int64 if rkey.dtype == torch.int64 else torch.int32
+        cap = max(1, skey.numel() if capacity is None else int(capacity))
+        for _ in range(2):
+            out_r = torch.empty(cap, dtype=dt, device=self.device)
+            out_s = torch.empty(cap, dtype=dt, device=self.device)
+            cnt = self.probe_relation(skey, spay, out_r, out_s, stream=stream)
+            m = int(cnt.item())
+            if m <= cap:
+                return out_r[:m], out_s[:m]
+            cap = m
+        raise RuntimeError("join output did not fit after resizing")
+
+
+# ------------------------------------------------------------------ datagen
+U64_MAX = (1 << 64) - 1
+
+
+def hit_threshold(frac: float) -> int:
+    if frac >= 1.0:
+        return U64_MAX
+    return min(U64_MAX - 1, int(frac * float(1 << 64)))
+
+
+def gen_pkfk(seed, NR, NS, frac=1.0, r0=0, nr=None, s0=0, ns=None, device=None, stream=None):
+    """Slice [r0, r0+nr) of R and [s0, s0+ns) of S of the PK-FK pair
+    (SURVEY 8(d) C1/C3), generated on the device."""
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    nr = NR if nr is None else nr
+    ns = NS if ns is None else ns
+    rk = torch.empty(nr, dtype=torch.int64, device=dev); rp = torch.empty_like(rk)
+    sk = torch.empty(ns, dtype=torch.int64, device=dev); sp = torch.empty_like(sk)
+    check(lib.hj_dev_gen_pkfk_i64(seed, NR, hit_threshold(frac), r0, nr, _ptr(rk), _ptr(rp), s0, ns, _ptr(sk),
+                                  _ptr(sp), _stream(dev, stream)), "hj_dev_gen_pkfk_i64")
+    return rk, rp, sk, sp
+
+
+def gen_uniform_i64(seed, stream_id, lo, hi, n, i0=0, device=None, stream=None):
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    k = torch.empty(n, dtype=torch.int64, device=dev); p = torch.empty_like(k)
+    check(lib.hj_dev_gen_uniform_i64(seed, stream_id, lo, hi, i0, n, _ptr(k), _ptr(p), _stream(dev, stream)),
+          "hj_dev_gen_uniform_i64")
+    return k, p
+
+
+def gen_uniform_i32(seed, stream_id, lo, hi, n, i0=0, device=None, stream=None):
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    k = torch.empty(n, dtype=torch.int32, device=dev)
+    check(lib.hj_dev_gen_uniform_i32(seed, stream_id, lo, hi, i0, n, _ptr(k), _stream(dev, stream)),
+          "hj_dev_gen_uniform_i32")
+    return k
+
+
+def partition_of(key: int, nparts: int) -> int:
+    """Owner of a key under the routing hash (host function of libhj.so)."""
+    return int(lib.hj_partition_of(int(key), int(nparts)))

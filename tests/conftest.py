@@ -1,0 +1,38 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "mlir-hashjoin_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP kernels)")
+    config.addinivalue_line("markers", "slow: full-size (2^26+) cases")
+
+
+def golden_cases(kind=None):
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))):
+        name = os.path.basename(f)[:-4]
+        if name == "nested_loop_kat":
+            continue
+        with np.load(f, allow_pickle=False) as z:
+            d = {k: z[k] for k in z.files}
+        if kind is None or int(d["kind"][0]) == kind:
+            out.append(pytest.param(d, id=name))
+    return out
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import pyoracle
+    pyoracle.lib()
+    return pyoracle
