@@ -27,6 +27,15 @@ _int = C.c_int
 
 
 def _load():
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so
+    # (SONAME libamdhip64.so.7) and loads it by path.  Importing torch first
+    # makes libhj.so's NEEDED libamdhip64.so.7 bind to that same instance
+    # (matched by SONAME); loading libhj.so first would map /opt/rocm's copy
+    # too, and two HSA runtimes in one process cannot share the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"libhj.so not found at {LIB_PATH}: build it with `make -C mlir-hashjoin_amd` "
