@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=22)
     ap.add_argument("--verify", action="store_true", help="check the last step's output properties")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "global", "radix"])
+    ap.add_argument("--radix-bits", type=int, default=0)
     return ap.parse_args()
 
 
@@ -108,14 +110,18 @@ def main():
         rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)
         sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 1 << 30, ns, i0=s0)
     hj = hashjoin.HashJoin(local)
+    hj.set_strategy(a.strategy, radix_bits=a.radix_bits)
     expect_m = NS if distn == "pkfk" else None
     torch.cuda.synchronize()
 
-    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "partition+exchange": 0.0}
+    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0,
+              "partition+exchange": 0.0}
     last = {}
 
     if world == 1:
         hj.allocate_hash_table(NR, 64)
+        hj.build_table(rk, rp)
+        hj.reserve_probe(NS, 64)
         cap = NS if distn == "pkfk" else int(NR * NS / (1 << 30) * 1.1) + 4096
         out_r = torch.empty(cap, dtype=torch.int64, device="cuda")
         out_s = torch.empty_like(out_r)
@@ -127,8 +133,8 @@ def main():
             hj.probe_relation(sk, sp, out_r, out_s, count=cnt)
             t = hj.last_timing()          # synchronises: the step ends with M known on the host
             if acc:
-                for k in ("init", "build", "probe"):
-                    phases[k] += t[k]
+                for k in ("init", "build", "probe", "probe_partition", "probe_join"):
+                    phases[k] += max(0.0, t[k])
             last["m"] = int(cnt.item())
     else:
         # strong scaling over the GLOBAL relations; output stays distributed
@@ -177,13 +183,16 @@ def main():
     value = NS / (ms / 1000.0)
     ph = {k: round(v / a.steps, 4) for k, v in phases.items() if v > 0}
 
-    # roofline of the dominant kernel (probe): algorithmic bytes per launch =
-    # |S_local| x (16 B stream S + 16 B one slot read) + M_local x 16 B output
-    # (SURVEY 8(d)), over the probe kernel's average HIP-event duration.
+    # Roofline of the dominant kernel sequence, the probe phase: algorithmic
+    # bytes per launch = |S_local| x (16 B stream S + 16 B one slot read) +
+    # M_local x 16 B output (SURVEY 8(d), 48 B per probe row at f = 1), over
+    # the probe phase's average HIP-event duration on the launch stream.
     probe_ms = phases["probe"] / a.steps
     probe_bytes = ns * 32 + m_local * 16
     achieved = probe_bytes / (probe_ms / 1000.0) / 1e9 if probe_ms > 0 else None
-    build_ms = phases["build"] / a.steps
+    build_ms = (phases["init"] + phases["build"]) / a.steps
+    join_ms = phases["probe_join"] / a.steps
+    strategy = hj.strategy_used or a.strategy
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),
@@ -203,8 +212,10 @@ def main():
         "joined_rows_per_sec": round(m_total / (ms / 1000.0), 1),
         "result_rows": m_total,
         "phase_ms": ph,
+        "strategy": strategy,
         "roofline": {
-            "kernel": "k_probe (hj_kernels.hip)",
+            "kernel": ("probe phase: S radix partition (k_hist+k_scatter per pass) + k_join" if strategy == "radix"
+                       else "k_probe (hj_kernels.hip)"),
             "bound": "hbm",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
@@ -215,10 +226,14 @@ def main():
             "avg_launch_ms": round(probe_ms, 4),
         },
         "build_roofline": {
-            "kernel": "k_build",
+            "kernel": "R radix partition" if strategy == "radix" else "k_init + k_build",
             "achieved": round(nr * 32 / (build_ms / 1000.0) / 1e9, 1) if build_ms > 0 else None,
             "unit": "GB/s", "algorithmic_bytes_per_launch": nr * 32, "avg_launch_ms": round(build_ms, 4),
         },
+        "join_kernel": None if strategy != "radix" or join_ms <= 0 else {
+            "kernel": "k_join (hj_radix.hip)", "avg_launch_ms": round(join_ms, 4),
+            "algorithmic_bytes_per_launch": (nr + ns) * 16 + m_local * 16,
+            "achieved": round(((nr + ns) * 16 + m_local * 16) / (join_ms / 1000.0) / 1e9, 1), "unit": "GB/s"},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))

@@ -69,14 +69,35 @@ void hj_ctx_destroy(hj_ctx *ctx);
 /* Size the workspace for builds of up to max_build_rows rows with 32- or
  * 64-bit keys (key_bits = 32 | 64). */
 int hj_ctx_reserve(hj_ctx *ctx, int64_t max_build_rows, int key_bits);
-/* Slot capacity of the current table (power of two, >= 2 x build rows). */
+/* Probe-side workspace of the radix strategy (no-op for the global table). */
+int hj_ctx_reserve_probe(hj_ctx *ctx, int64_t max_probe_rows, int key_bits);
+/* Join strategy.  GLOBAL: one linear-probing table in HBM (build = 64-bit CAS
+ * per row, probe = random slot reads).  RADIX: both relations radix-
+ * partitioned by the key hash until a partition's build rows fit an LDS
+ * table; partitions are joined in LDS.  AUTO picks RADIX for large build
+ * sides.  The result multiset is identical. */
+#define HJ_STRATEGY_AUTO 0
+#define HJ_STRATEGY_GLOBAL 1
+#define HJ_STRATEGY_RADIX 2
+int hj_ctx_set_strategy(hj_ctx *ctx, int strategy);
+/* RADIX: partition into exactly 2^bits partitions (1..24; 0 = planner's
+ * choice, ~4096 build rows per partition).  For tests and tuning. */
+int hj_ctx_set_radix_bits(hj_ctx *ctx, int bits);
+/* Strategy the current build uses (HJ_STRATEGY_GLOBAL / _RADIX), 0 if none. */
+int hj_ctx_strategy_used(const hj_ctx *ctx);
+/* GLOBAL: slot capacity of the table (power of two, >= 2 x build rows);
+ * RADIX: number of partitions. */
 int64_t hj_ctx_table_capacity(const hj_ctx *ctx);
-/* 1 if the last build saw a duplicate key, 0 if not (synchronises). */
+/* 1 if the build side repeats a key, 0 if not (synchronises).  Known after
+ * the build (GLOBAL) or after the first probe (RADIX). */
 int hj_ctx_build_has_duplicates(hj_ctx *ctx);
 /* Per-phase kernel timing with HIP events on the caller's stream. */
 int hj_ctx_set_timing(hj_ctx *ctx, int enable);
 /* ms of the last init, build, probe/count and partition launches (synchronises). */
 int hj_ctx_last_timing(hj_ctx *ctx, float ms[4]);
+/* Same plus the probe's split: [4] probe-side partitioning (RADIX, else 0),
+ * [5] probe/join kernel; [6], [7] reserved (-1). */
+int hj_ctx_last_timing_ex(hj_ctx *ctx, float ms[8]);
 
 /* ------------------------------------------------------------ device phases
  * build:  @initializeHashTable + @buildTable   (join_v2.mlir:54-108)

@@ -61,7 +61,16 @@ int table_bits(int64_t n) {
     return b < 4 ? 4 : b;
 }
 
-enum Ev { kEvInit0, kEvInit1, kEvBuild1, kEvProbe0, kEvProbe1, kEvPart0, kEvPart1, kEvCount };
+enum Ev { kEvInit0, kEvInit1, kEvBuild1, kEvProbe0, kEvProbeMid, kEvProbe1, kEvPart0, kEvPart1, kEvCount };
+
+// Build sides at least this large use the radix-partitioned join (LDS
+// tables); smaller ones a global linear-probing table (HJ_STRATEGY_AUTO).
+constexpr int64_t kRadixMinRows = 1ll << 21;
+
+struct Buf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
 
 }  // namespace
 
@@ -77,11 +86,18 @@ struct hj_ctx {
     int layout = -1;
     int bits = 0;
     int64_t n_build = 0;
+    int strategy = HJ_STRATEGY_AUTO;   // requested
+    int radix_bits = 0;                // 0: planner chooses
+    int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
+    // radix-join workspace (hj_radix.hip)
+    hj::RadixPlan plan;
+    Buf rk, rp, sk, sp, tk, tp, off_a, off_b, r_off, s_off, tile_start, work_start, hist, scan_sums;
     // timing
     bool timing = false;
     bool ev_ready = false;
     hipEvent_t ev[kEvCount];
     bool rec[4] = {false, false, false, false};
+    bool rec_mid = false;
     // host memref path
     hipStream_t host_stream = nullptr;
     void *dbuf[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -141,16 +157,91 @@ void record(hj_ctx *c, int ev, hipStream_t st) {
     if (c->timing && c->ev_ready) (void)hipEventRecord(c->ev[ev], st);
 }
 
+int ensure_buf(Buf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return HJ_OK;
+    if (b.p) HJ_HIP(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc radix workspace " + std::to_string(bytes));
+    b.bytes = bytes;
+    return HJ_OK;
+}
+
+void free_buf(Buf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+}
+
+// Partition scratch sized for n rows under plan pl (shared by R and S).
+int ensure_radix_scratch(hj_ctx *c, int64_t n, size_t esz, const hj::RadixPlan &pl) {
+    const size_t P = size_t(1) << pl.total_bits;
+    const size_t rows = (size_t)(n > 0 ? n : 1);
+    if (pl.passes > 1) {
+        HJ_TRY(ensure_buf(c->tk, rows * esz));
+        HJ_TRY(ensure_buf(c->tp, rows * esz));
+    }
+    HJ_TRY(ensure_buf(c->off_a, (P + 1) * 8));
+    HJ_TRY(ensure_buf(c->off_b, (P + 1) * 8));
+    HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
+    HJ_TRY(ensure_buf(c->work_start, (P + 1) * 4));
+    const size_t he = hj::radix_hist_elems(n, (int)P);
+    HJ_TRY(ensure_buf(c->hist, he * 8));
+    HJ_TRY(ensure_buf(c->scan_sums, (he / 8192 + 2) * 8));
+    return HJ_OK;
+}
+
+hj::RadixWork radix_work(hj_ctx *c) {
+    hj::RadixWork w;
+    w.tmp_key = c->tk.p;
+    w.tmp_pay = c->tp.p;
+    w.off_a = (unsigned long long *)c->off_a.p;
+    w.off_b = (unsigned long long *)c->off_b.p;
+    w.tile_start = (unsigned *)c->tile_start.p;
+    w.hist = (unsigned long long *)c->hist.p;
+    w.scan_sums = (unsigned long long *)c->scan_sums.p;
+    return w;
+}
+
+int choose_strategy(const hj_ctx *c, int64_t n_build) {
+    if (c->strategy == HJ_STRATEGY_GLOBAL || c->strategy == HJ_STRATEGY_RADIX) return c->strategy;
+    return n_build >= kRadixMinRows ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
+}
+
 int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     if (src.n < 0 || (src.n > 0 && !src.key) || (src.form == hj::kCols64 && src.n > 0 && !src.pay))
         HJ_FAIL(HJ_ERR_ARG, "bad build relation");
     if (layout == kNarrow && src.n > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids: build side must have < 2^31 rows");
     HJ_TRY(set_device(c));
-    HJ_TRY(ensure_table(c, src.n, layout));
+    HJ_TRY(ensure_meta(c, 64));
     c->layout = layout;
-    c->bits = table_bits(src.n);
     c->n_build = src.n;
+    c->used = choose_strategy(c, src.n);
+    if (c->used == HJ_STRATEGY_RADIX) {
+        // build = radix-partition R by the top key-hash bits (tables are built
+        // per partition in LDS at probe time)
+        const bool wide = layout == kWide;
+        const size_t esz = wide ? 8 : 4;
+        c->plan = hj::radix_plan(src.n, c->radix_bits);
+        const size_t P = size_t(1) << c->plan.total_bits;
+        const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
+        HJ_TRY(ensure_buf(c->rk, rows * esz));
+        HJ_TRY(ensure_buf(c->rp, rows * esz));
+        HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
+        HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
+        record(c, kEvInit0, st);
+        HJ_HIP(hipMemsetAsync(c->meta, 0, 2 * sizeof(unsigned long long), st));
+        record(c, kEvInit1, st);
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->rk.p, c->rp.p,
+                                   (unsigned long long *)c->r_off.p, st));
+        record(c, kEvBuild1, st);
+        c->rec[0] = c->rec[1] = c->timing;
+        return HJ_OK;
+    }
+    HJ_TRY(ensure_table(c, src.n, layout));
+    c->bits = table_bits(src.n);
     const hj::TableDev t = table_dev(c);
     record(c, kEvInit0, st);
     HJ_HIP(hj::launch_init(t, layout, 1ull << c->bits, st));
@@ -170,6 +261,28 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     if (!count_only && (cap < 0 || (cap > 0 && (!out_r || !out_s)))) HJ_FAIL(HJ_ERR_ARG, "bad output");
     HJ_TRY(set_device(c));
     HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+    if (c->used == HJ_STRATEGY_RADIX) {
+        const bool wide = layout == kWide;
+        const size_t esz = wide ? 8 : 4;
+        const size_t P = size_t(1) << c->plan.total_bits;
+        const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
+        HJ_TRY(ensure_buf(c->sk, rows * esz));
+        HJ_TRY(ensure_buf(c->sp, rows * esz));
+        HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
+        HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
+        record(c, kEvProbe0, st);
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->sk.p, c->sp.p,
+                                   (unsigned long long *)c->s_off.p, st));
+        record(c, kEvProbeMid, st);
+        HJ_HIP(hj::radix_join(wide, c->plan, c->rk.p, c->rp.p, (const unsigned long long *)c->r_off.p, c->sk.p,
+                              c->sp.p, (const unsigned long long *)c->s_off.p, src.n, (unsigned *)c->work_start.p,
+                              out_r, out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1,
+                              count_only, st));
+        record(c, kEvProbe1, st);
+        c->rec[2] = c->timing;
+        c->rec_mid = c->timing;
+        return HJ_OK;
+    }
     hj::OutDev out;
     out.r = out_r;
     out.s = out_s;
@@ -179,6 +292,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, st));
     record(c, kEvProbe1, st);
     c->rec[2] = c->timing;
+    c->rec_mid = false;
     return HJ_OK;
 }
 
@@ -454,6 +568,9 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (int i = 0; i < 6; ++i)
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
+    for (Buf *b : {&c->rk, &c->rp, &c->sk, &c->sp, &c->tk, &c->tp, &c->off_a, &c->off_b, &c->r_off, &c->s_off,
+                   &c->tile_start, &c->work_start, &c->hist, &c->scan_sums})
+        free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
     {
@@ -471,10 +588,24 @@ int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     if (max_build_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
     HJ_TRY(set_device(c));
-    return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
+    HJ_TRY(ensure_meta(c, 64));
+    if (choose_strategy(c, max_build_rows) == HJ_STRATEGY_GLOBAL)
+        return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
+    const size_t esz = key_bits == 64 ? 8 : 4;
+    const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits);
+    const size_t P = size_t(1) << pl.total_bits;
+    const size_t rows = (size_t)(max_build_rows > 0 ? max_build_rows : 1);
+    HJ_TRY(ensure_buf(c->rk, rows * esz));
+    HJ_TRY(ensure_buf(c->rp, rows * esz));
+    HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
+    return ensure_radix_scratch(c, max_build_rows, esz, pl);
 }
 
-int64_t hj_ctx_table_capacity(const hj_ctx *c) { return (c && c->layout >= 0) ? (int64_t)(1ll << c->bits) : 0; }
+int64_t hj_ctx_table_capacity(const hj_ctx *c) {
+    if (!c || c->layout < 0) return 0;
+    if (c->used == HJ_STRATEGY_RADIX) return (int64_t)(1ll << c->plan.total_bits);   // partitions
+    return (int64_t)(1ll << c->bits);
+}
 
 int hj_ctx_build_has_duplicates(hj_ctx *c) {
     if (!c || c->layout < 0) HJ_FAIL(HJ_ERR_STATE, "no table built");
@@ -496,18 +627,68 @@ int hj_ctx_set_timing(hj_ctx *c, int enable) {
     return HJ_OK;
 }
 
-int hj_ctx_last_timing(hj_ctx *c, float ms[4]) {
+int hj_ctx_last_timing_ex(hj_ctx *c, float ms[8]) {
     if (!c || !ms) HJ_FAIL(HJ_ERR_ARG, "null argument");
-    for (int i = 0; i < 4; ++i) ms[i] = -1.0f;
+    for (int i = 0; i < 8; ++i) ms[i] = -1.0f;
     if (!c->ev_ready) return HJ_OK;
     HJ_TRY(set_device(c));
-    const int pairs[4][2] = {{kEvInit0, kEvInit1}, {kEvInit1, kEvBuild1}, {kEvProbe0, kEvProbe1}, {kEvPart0, kEvPart1}};
-    for (int i = 0; i < 4; ++i) {
-        if (!c->rec[i]) continue;
-        HJ_HIP(hipEventSynchronize(c->ev[pairs[i][1]]));
-        HJ_HIP(hipEventElapsedTime(&ms[i], c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
+    auto el = [&](int a, int b, float *out) -> int {
+        HJ_HIP(hipEventSynchronize(c->ev[b]));
+        HJ_HIP(hipEventElapsedTime(out, c->ev[a], c->ev[b]));
+        return HJ_OK;
+    };
+    if (c->rec[0]) HJ_TRY(el(kEvInit0, kEvInit1, &ms[0]));
+    if (c->rec[1]) HJ_TRY(el(kEvInit1, kEvBuild1, &ms[1]));
+    if (c->rec[2]) HJ_TRY(el(kEvProbe0, kEvProbe1, &ms[2]));
+    if (c->rec[3]) HJ_TRY(el(kEvPart0, kEvPart1, &ms[3]));
+    if (c->rec[2]) {
+        if (c->rec_mid) {
+            HJ_TRY(el(kEvProbe0, kEvProbeMid, &ms[4]));
+            HJ_TRY(el(kEvProbeMid, kEvProbe1, &ms[5]));
+        } else {
+            ms[4] = 0.0f;
+            ms[5] = ms[2];
+        }
     }
     return HJ_OK;
+}
+
+int hj_ctx_last_timing(hj_ctx *c, float ms[4]) {
+    float ex[8];
+    HJ_TRY(hj_ctx_last_timing_ex(c, ex));
+    for (int i = 0; i < 4; ++i) ms[i] = ex[i];
+    return HJ_OK;
+}
+
+int hj_ctx_set_strategy(hj_ctx *c, int strategy) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (strategy != HJ_STRATEGY_AUTO && strategy != HJ_STRATEGY_GLOBAL && strategy != HJ_STRATEGY_RADIX)
+        HJ_FAIL(HJ_ERR_ARG, "unknown strategy");
+    c->strategy = strategy;
+    return HJ_OK;
+}
+
+int hj_ctx_set_radix_bits(hj_ctx *c, int bits) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (bits < 0 || bits > 24) HJ_FAIL(HJ_ERR_ARG, "radix bits must be in [0, 24]");
+    c->radix_bits = bits;
+    return HJ_OK;
+}
+
+int hj_ctx_strategy_used(const hj_ctx *c) { return (c && c->layout >= 0) ? c->used : 0; }
+
+int hj_ctx_reserve_probe(hj_ctx *c, int64_t max_probe_rows, int key_bits) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (max_probe_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
+    if (c->layout < 0 || c->used != HJ_STRATEGY_RADIX) return HJ_OK;   // the global table needs no probe workspace
+    HJ_TRY(set_device(c));
+    const size_t esz = key_bits == 64 ? 8 : 4;
+    const size_t P = size_t(1) << c->plan.total_bits;
+    const size_t rows = (size_t)(max_probe_rows > 0 ? max_probe_rows : 1);
+    HJ_TRY(ensure_buf(c->sk, rows * esz));
+    HJ_TRY(ensure_buf(c->sp, rows * esz));
+    HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
+    return ensure_radix_scratch(c, max_probe_rows, esz, c->plan);
 }
 
 // ------------------------------------------------------------ device phases

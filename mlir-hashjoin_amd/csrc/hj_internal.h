@@ -66,6 +66,34 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
                         bool count_only, hipStream_t st);
 
+// ---------------------------------------------------------------- radix join
+// (hj_radix.hip) partitions both relations by the top bits of the key hash
+// until a partition's build rows fit one workgroup's LDS table, then joins
+// partition pairs in LDS.
+struct RadixPlan {
+    int passes;       // 1..3 partition passes
+    int bits[3];      // fan-out bits per pass (<= 8 each)
+    int total_bits;   // P = 2^total_bits partitions
+};
+
+struct RadixWork {                 // scratch shared by the partition passes
+    void *tmp_key, *tmp_pay;       // ping buffer (multi-pass plans), >= n rows
+    unsigned long long *off_a, *off_b;   // segment offsets, >= 2^total_bits + 1
+    unsigned *tile_start;          // >= 2^total_bits + 1
+    unsigned long long *hist;      // >= radix_hist_elems(n, 2^total_bits)
+    unsigned long long *scan_sums; // >= hist elems / 8192 + 1
+};
+
+RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0: fixed 2^bits partitions
+size_t radix_hist_elems(long long n, int max_nseg);
+int radix_chunk_rows();
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out_key,
+                           void *out_pay, unsigned long long *out_off, hipStream_t st);
+hipError_t radix_join(bool wide, const RadixPlan &pl, const void *rk, const void *rp, const unsigned long long *r_off,
+                      const void *sk, const void *sp, const unsigned long long *s_off, long long n_s,
+                      unsigned *work_start, void *out_r, void *out_s, long long cap, unsigned long long *counter,
+                      unsigned long long *dup_flag, bool count_only, hipStream_t st);
+
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
                             hipStream_t st);

@@ -20,6 +20,10 @@ HJ_ERR_NOMEM = -3
 HJ_ERR_STATE = -4
 HJ_ERR_CAPACITY = -5
 
+HJ_STRATEGY_AUTO = 0
+HJ_STRATEGY_GLOBAL = 1
+HJ_STRATEGY_RADIX = 2
+
 _vp = C.c_void_p
 _i64 = C.c_int64
 _u64 = C.c_uint64
@@ -51,6 +55,11 @@ def _load():
         "hj_ctx_build_has_duplicates": (_int, [_vp]),
         "hj_ctx_set_timing": (_int, [_vp, _int]),
         "hj_ctx_last_timing": (_int, [_vp, C.POINTER(C.c_float)]),
+        "hj_ctx_last_timing_ex": (_int, [_vp, C.POINTER(C.c_float)]),
+        "hj_ctx_reserve_probe": (_int, [_vp, _i64, _int]),
+        "hj_ctx_set_strategy": (_int, [_vp, _int]),
+        "hj_ctx_strategy_used": (_int, [_vp]),
+        "hj_ctx_set_radix_bits": (_int, [_vp, _int]),
         "hj_dev_build_i64": (_int, [_vp, _vp, _vp, _i64, _vp]),
         "hj_dev_count_i64": (_int, [_vp, _vp, _i64, _vp, _vp]),
         "hj_dev_probe_i64": (_int, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),

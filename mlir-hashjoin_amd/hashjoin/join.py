@@ -20,7 +20,9 @@ import ctypes as C
 
 import torch
 
-from ._lib import check, lib
+from ._lib import HJ_STRATEGY_AUTO, HJ_STRATEGY_GLOBAL, HJ_STRATEGY_RADIX, check, lib
+
+STRATEGIES = {"auto": HJ_STRATEGY_AUTO, "global": HJ_STRATEGY_GLOBAL, "radix": HJ_STRATEGY_RADIX}
 
 
 def _ptr(t):
@@ -67,6 +69,20 @@ class HashJoin:
         """@allocateHashTable (join_v2.mlir:25-39): size the workspace once."""
         check(lib.hj_ctx_reserve(self._ctx, int(num_tuples), int(key_bits)), "hj_ctx_reserve")
 
+    def reserve_probe(self, num_tuples, key_bits=64):
+        check(lib.hj_ctx_reserve_probe(self._ctx, int(num_tuples), int(key_bits)), "hj_ctx_reserve_probe")
+
+    def set_strategy(self, name, radix_bits=0):
+        """'auto' | 'global' (one HBM table) | 'radix' (partitioned, LDS tables);
+        radix_bits > 0 fixes the partition count to 2^radix_bits."""
+        check(lib.hj_ctx_set_strategy(self._ctx, STRATEGIES[name]), "hj_ctx_set_strategy")
+        check(lib.hj_ctx_set_radix_bits(self._ctx, int(radix_bits)), "hj_ctx_set_radix_bits")
+
+    @property
+    def strategy_used(self):
+        return {HJ_STRATEGY_GLOBAL: "global", HJ_STRATEGY_RADIX: "radix"}.get(
+            lib.hj_ctx_strategy_used(self._ctx), None)
+
     @property
     def capacity(self):
         return int(lib.hj_ctx_table_capacity(self._ctx))
@@ -81,10 +97,11 @@ class HashJoin:
         check(lib.hj_ctx_set_timing(self._ctx, 1 if enable else 0), "hj_ctx_set_timing")
 
     def last_timing(self):
-        """ms of the last (init, build, probe/count, partition) launches."""
-        a = (C.c_float * 4)()
-        check(lib.hj_ctx_last_timing(self._ctx, a), "hj_ctx_last_timing")
-        return dict(zip(("init", "build", "probe", "partition"), list(a)))
+        """ms of the last (init, build, probe, routing partition) launches and
+        the probe's split into probe-side partitioning and the join kernel."""
+        a = (C.c_float * 8)()
+        check(lib.hj_ctx_last_timing_ex(self._ctx, a), "hj_ctx_last_timing_ex")
+        return dict(zip(("init", "build", "probe", "partition", "probe_partition", "probe_join"), list(a)[:6]))
 
     # -------------------------------------------------------------- phases
     def build_table(self, rkey, rpay=None, row_base=0, stream=None):

@@ -1,0 +1,149 @@
+"""GPU parity of the radix-partitioned strategy (hj_radix.hip) vs the oracle.
+
+The partition count is forced (hj_ctx_set_radix_bits) so 1-, 2- and 3-pass
+plans, empty partitions, oversized partitions (several LDS build rounds) and
+the INT64_MIN side path are all exercised at sizes the oracle checks exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+import hashjoin
+from hashjoin import HashJoin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hj():
+    h = HashJoin(0)
+    yield h
+    h.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run(hj, rk, rp, sk, sp, bits, capacity=None):
+    hj.set_strategy("radix", radix_bits=bits)
+    try:
+        if rk.dtype == np.int32:
+            o_r, o_s = hj.join(dev(rk), None, dev(sk), None, capacity=capacity)
+        else:
+            o_r, o_s = hj.join(dev(rk), dev(rp), dev(sk), dev(sp), capacity=capacity)
+        assert hj.strategy_used == "radix"
+        torch.cuda.synchronize()
+        return o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64)
+    finally:
+        hj.set_strategy("auto")
+
+
+@pytest.mark.parametrize("bits", [1, 3, 8, 9, 12, 16, 17])   # 1-pass ... 3-pass plans
+def test_radix_pkfk_vs_oracle(hj, oracle, bits):
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(bits, 20000, 30000, 0.7)
+    o = run(hj, rk, rp * 5 - 1, sk, sp, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp * 5 - 1, sk, sp, H=200))
+
+
+@pytest.mark.parametrize("bits", [2, 10])
+def test_radix_duplicates_both_sides(hj, oracle, bits):
+    rk, rp = oracle.gen_uniform_i64(bits, 1, 1, 500, 12000)
+    sk, sp = oracle.gen_uniform_i64(bits, 2, 1, 500, 9000)
+    o = run(hj, rk, rp, sk, sp, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=50))
+    assert hj.has_duplicates()
+
+
+def test_radix_oversized_partition_rounds(hj, oracle):
+    """20000 build rows of ONE key land in one partition: > 5120 rows per LDS
+    round, so the join runs several build rounds and still emits every pair."""
+    rk = np.concatenate([np.full(20000, 42, np.int64), np.arange(1000, 3000, dtype=np.int64)])
+    rp = np.arange(len(rk), dtype=np.int64)
+    sk = np.array([42, 7, 42, 2500, 99999], np.int64); sp = np.arange(5, dtype=np.int64) + 10
+    o = run(hj, rk, rp, sk, sp, 4)
+    assert len(o[0]) == 2 * 20000 + 1
+    assert oracle.same_multiset(*o, *oracle.nested_loop_i64(rk, rp, sk, sp))
+
+
+def test_radix_big_probe_chunks(hj, oracle):
+    """A hot probe key: one partition's S rows span many 8192-row chunks."""
+    rk = np.arange(3000, dtype=np.int64) * 7; rp = np.arange(3000, dtype=np.int64)
+    sk = np.concatenate([np.full(50000, 21, np.int64), np.arange(0, 30000, 3, dtype=np.int64)])
+    sp = np.arange(len(sk), dtype=np.int64)
+    o = run(hj, rk, rp, sk, sp, 6)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=300))
+
+
+def test_radix_int64_min_keys(hj, oracle):
+    I64_MIN = -(1 << 63)
+    rk, rp = oracle.gen_uniform_i64(3, 1, -100, 100, 5000)
+    sk, sp = oracle.gen_uniform_i64(3, 2, -100, 100, 4000)
+    rk[::97] = I64_MIN; sk[::131] = I64_MIN
+    o = run(hj, rk, rp, sk, sp, 5)
+    assert oracle.same_multiset(*o, *oracle.nested_loop_i64(rk, rp, sk, sp))
+
+
+@pytest.mark.parametrize("bits", [1, 9])
+def test_radix_i32_reference_types(hj, oracle, bits):
+    r = oracle.gen_uniform_i32(bits, 1, -(1 << 31), (1 << 31) - 1, 30000)
+    s = np.concatenate([r[::3], oracle.gen_uniform_i32(bits, 2, 1, 1000, 10000)])
+    o = run(hj, r, None, s, None, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i32(r, s, H=300))
+
+
+def test_radix_empty_and_tiny(hj, oracle):
+    e = np.empty(0, np.int64)
+    k, p = oracle.gen_uniform_i64(1, 1, 1, 5, 10)
+    for rk, rp, sk, sp in [(k, p, e, e), (e, e, k, p), (k[:1], p[:1], k[:1], p[:1])]:
+        hj.set_strategy("radix", radix_bits=3)
+        hj.build_table(torch.tensor(rk, dtype=torch.int64, device="cuda"), torch.tensor(rp, dtype=torch.int64, device="cuda"))
+        out_r = torch.empty(64, dtype=torch.int64, device="cuda"); out_s = torch.empty_like(out_r)
+        cnt = hj.probe_relation(torch.tensor(sk, dtype=torch.int64, device="cuda"),
+                                torch.tensor(sp, dtype=torch.int64, device="cuda"), out_r, out_s)
+        m = int(cnt.item())
+        exp = oracle.nested_loop_i64(rk, rp, sk, sp)
+        assert oracle.same_multiset(out_r.cpu().numpy()[:m], out_s.cpu().numpy()[:m], *exp)
+    hj.set_strategy("auto")
+
+
+def test_radix_count_and_capacity(hj, oracle):
+    rk, rp = oracle.gen_uniform_i64(9, 1, 1, 2000, 40000)
+    sk, sp = oracle.gen_uniform_i64(9, 2, 1, 2000, 40000)
+    exp = oracle.nested_loop_i64(rk, rp, sk, sp)
+    hj.set_strategy("radix", radix_bits=7)
+    hj.build_table(dev(rk), dev(rp))
+    assert hj.count_rows(dev(sk)) == len(exp[0])
+    out_r = torch.empty(1000, dtype=torch.int64, device="cuda"); out_s = torch.empty_like(out_r)
+    assert int(hj.probe_relation(dev(sk), dev(sp), out_r, out_s).item()) == len(exp[0])
+    hj.set_strategy("auto")
+    o = run(hj, rk, rp, sk, sp, 7, capacity=5)
+    assert oracle.same_multiset(*o, *exp)
+
+
+def test_strategies_agree_full_size(hj):
+    """C1 at 2^24: global and radix strategies give the same pair set."""
+    n = 1 << 24
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EED, n, n, 0.9)
+    outs = []
+    for strat in ("global", "radix"):
+        hj.set_strategy(strat)
+        o_r, o_s = hj.join(rk, rp, sk, sp)
+        assert hj.strategy_used == strat
+        order = torch.argsort(o_s)
+        outs.append((o_r[order], o_s[order]))
+    hj.set_strategy("auto")
+    assert outs[0][0].numel() == outs[1][0].numel()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.slow
+def test_radix_c3_2p28(hj):
+    n = 1 << 28
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EED, n, n)
+    hj.set_strategy("radix")
+    o_r, o_s = hj.join(rk, rp, sk, sp)
+    hj.set_strategy("auto")
+    assert o_r.numel() == n
+    assert bool((rk[o_r] == sk[o_s]).all())
+    assert torch.equal(torch.sort(o_s)[0], torch.arange(n, device="cuda"))
