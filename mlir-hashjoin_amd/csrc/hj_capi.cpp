@@ -91,7 +91,7 @@ struct hj_ctx {
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
-    Buf rk, rp, sk, sp, tk, tp, off_a, off_b, r_off, s_off, tile_start, work_start, hist, scan_sums;
+    Buf rrows, srows, tmp, off_a, off_b, r_off, s_off, tile_start, tile_owner, work_start, hist, scan_sums;
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -178,14 +178,13 @@ void free_buf(Buf &b) {
 int ensure_radix_scratch(hj_ctx *c, int64_t n, size_t esz, const hj::RadixPlan &pl) {
     const size_t P = size_t(1) << pl.total_bits;
     const size_t rows = (size_t)(n > 0 ? n : 1);
-    if (pl.passes > 1) {
-        HJ_TRY(ensure_buf(c->tk, rows * esz));
-        HJ_TRY(ensure_buf(c->tp, rows * esz));
-    }
+    if (pl.passes > 1) HJ_TRY(ensure_buf(c->tmp, rows * esz));
     HJ_TRY(ensure_buf(c->off_a, (P + 1) * 8));
     HJ_TRY(ensure_buf(c->off_b, (P + 1) * 8));
     HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
-    HJ_TRY(ensure_buf(c->work_start, (P + 1) * 4));
+    HJ_TRY(ensure_buf(c->tile_owner, ((size_t)(n > 0 ? n : 1) / 4096 + P + 2) * 4));
+    // work map: P + 1 chunk starts, then the item -> partition owner list
+    HJ_TRY(ensure_buf(c->work_start, (P + 1 + (size_t)(n > 0 ? n : 1) / (size_t)hj::radix_chunk_rows() + P + 2) * 4));
     const size_t he = hj::radix_hist_elems(n, (int)P);
     HJ_TRY(ensure_buf(c->hist, he * 8));
     HJ_TRY(ensure_buf(c->scan_sums, (he / 8192 + 2) * 8));
@@ -194,11 +193,11 @@ int ensure_radix_scratch(hj_ctx *c, int64_t n, size_t esz, const hj::RadixPlan &
 
 hj::RadixWork radix_work(hj_ctx *c) {
     hj::RadixWork w;
-    w.tmp_key = c->tk.p;
-    w.tmp_pay = c->tp.p;
+    w.tmp = c->tmp.p;
     w.off_a = (unsigned long long *)c->off_a.p;
     w.off_b = (unsigned long long *)c->off_b.p;
     w.tile_start = (unsigned *)c->tile_start.p;
+    w.tile_owner = (unsigned *)c->tile_owner.p;
     w.hist = (unsigned long long *)c->hist.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
     return w;
@@ -223,19 +222,18 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         // build = radix-partition R by the top key-hash bits (tables are built
         // per partition in LDS at probe time)
         const bool wide = layout == kWide;
-        const size_t esz = wide ? 8 : 4;
+        const size_t esz = wide ? 16 : 8;   // packed partitioned rows
         c->plan = hj::radix_plan(src.n, c->radix_bits);
         const size_t P = size_t(1) << c->plan.total_bits;
         const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
-        HJ_TRY(ensure_buf(c->rk, rows * esz));
-        HJ_TRY(ensure_buf(c->rp, rows * esz));
+        HJ_TRY(ensure_buf(c->rrows, rows * esz));
         HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
         HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
         record(c, kEvInit0, st);
         HJ_HIP(hipMemsetAsync(c->meta, 0, 2 * sizeof(unsigned long long), st));
         record(c, kEvInit1, st);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->rk.p, c->rp.p,
-                                   (unsigned long long *)c->r_off.p, st));
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->rrows.p, (unsigned long long *)c->r_off.p,
+                                   st));
         record(c, kEvBuild1, st);
         c->rec[0] = c->rec[1] = c->timing;
         return HJ_OK;
@@ -263,21 +261,20 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
     if (c->used == HJ_STRATEGY_RADIX) {
         const bool wide = layout == kWide;
-        const size_t esz = wide ? 8 : 4;
+        const size_t esz = wide ? 16 : 8;
         const size_t P = size_t(1) << c->plan.total_bits;
         const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
-        HJ_TRY(ensure_buf(c->sk, rows * esz));
-        HJ_TRY(ensure_buf(c->sp, rows * esz));
+        HJ_TRY(ensure_buf(c->srows, rows * esz));
         HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
         HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
         record(c, kEvProbe0, st);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->sk.p, c->sp.p,
-                                   (unsigned long long *)c->s_off.p, st));
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->srows.p, (unsigned long long *)c->s_off.p,
+                                   st));
         record(c, kEvProbeMid, st);
-        HJ_HIP(hj::radix_join(wide, c->plan, c->rk.p, c->rp.p, (const unsigned long long *)c->r_off.p, c->sk.p,
-                              c->sp.p, (const unsigned long long *)c->s_off.p, src.n, (unsigned *)c->work_start.p,
-                              out_r, out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1,
-                              count_only, st));
+        HJ_HIP(hj::radix_join(wide, c->plan, c->rrows.p, (const unsigned long long *)c->r_off.p, c->srows.p,
+                              (const unsigned long long *)c->s_off.p, src.n, (unsigned *)c->work_start.p, out_r,
+                              out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1, count_only,
+                              st));
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
         c->rec_mid = c->timing;
@@ -568,8 +565,8 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (int i = 0; i < 6; ++i)
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
-    for (Buf *b : {&c->rk, &c->rp, &c->sk, &c->sp, &c->tk, &c->tp, &c->off_a, &c->off_b, &c->r_off, &c->s_off,
-                   &c->tile_start, &c->work_start, &c->hist, &c->scan_sums})
+    for (Buf *b : {&c->rrows, &c->srows, &c->tmp, &c->off_a, &c->off_b, &c->r_off, &c->s_off,
+                   &c->tile_start, &c->tile_owner, &c->work_start, &c->hist, &c->scan_sums})
         free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -591,12 +588,11 @@ int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
     HJ_TRY(ensure_meta(c, 64));
     if (choose_strategy(c, max_build_rows) == HJ_STRATEGY_GLOBAL)
         return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
-    const size_t esz = key_bits == 64 ? 8 : 4;
+    const size_t esz = key_bits == 64 ? 16 : 8;
     const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits);
     const size_t P = size_t(1) << pl.total_bits;
     const size_t rows = (size_t)(max_build_rows > 0 ? max_build_rows : 1);
-    HJ_TRY(ensure_buf(c->rk, rows * esz));
-    HJ_TRY(ensure_buf(c->rp, rows * esz));
+    HJ_TRY(ensure_buf(c->rrows, rows * esz));
     HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
     return ensure_radix_scratch(c, max_build_rows, esz, pl);
 }
@@ -682,11 +678,10 @@ int hj_ctx_reserve_probe(hj_ctx *c, int64_t max_probe_rows, int key_bits) {
     if (max_probe_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
     if (c->layout < 0 || c->used != HJ_STRATEGY_RADIX) return HJ_OK;   // the global table needs no probe workspace
     HJ_TRY(set_device(c));
-    const size_t esz = key_bits == 64 ? 8 : 4;
+    const size_t esz = key_bits == 64 ? 16 : 8;
     const size_t P = size_t(1) << c->plan.total_bits;
     const size_t rows = (size_t)(max_probe_rows > 0 ? max_probe_rows : 1);
-    HJ_TRY(ensure_buf(c->sk, rows * esz));
-    HJ_TRY(ensure_buf(c->sp, rows * esz));
+    HJ_TRY(ensure_buf(c->srows, rows * esz));
     HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
     return ensure_radix_scratch(c, max_probe_rows, esz, c->plan);
 }

@@ -77,9 +77,10 @@ struct RadixPlan {
 };
 
 struct RadixWork {                 // scratch shared by the partition passes
-    void *tmp_key, *tmp_pay;       // ping buffer (multi-pass plans), >= n rows
+    void *tmp;                     // ping buffer of packed rows (multi-pass plans), >= n rows
     unsigned long long *off_a, *off_b;   // segment offsets, >= 2^total_bits + 1
     unsigned *tile_start;          // >= 2^total_bits + 1
+    unsigned *tile_owner;          // >= n / 4096 + 2^total_bits + 1
     unsigned long long *hist;      // >= radix_hist_elems(n, 2^total_bits)
     unsigned long long *scan_sums; // >= hist elems / 8192 + 1
 };
@@ -87,11 +88,12 @@ struct RadixWork {                 // scratch shared by the partition passes
 RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0: fixed 2^bits partitions
 size_t radix_hist_elems(long long n, int max_nseg);
 int radix_chunk_rows();
-hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out_key,
-                           void *out_pay, unsigned long long *out_off, hipStream_t st);
-hipError_t radix_join(bool wide, const RadixPlan &pl, const void *rk, const void *rp, const unsigned long long *r_off,
-                      const void *sk, const void *sp, const unsigned long long *s_off, long long n_s,
-                      unsigned *work_start, void *out_r, void *out_s, long long cap, unsigned long long *counter,
+// Partitioned rows are packed: 16 B {key, pay} (wide) or 8 B key << 32 | row id (narrow).
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out,
+                           unsigned long long *out_off, hipStream_t st);
+hipError_t radix_join(bool wide, const RadixPlan &pl, const void *r_rows, const unsigned long long *r_off,
+                      const void *s_rows, const unsigned long long *s_off, long long n_s, unsigned *work_start,
+                      void *out_r, void *out_s, long long cap, unsigned long long *counter,
                       unsigned long long *dup_flag, bool count_only, hipStream_t st);
 
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,

@@ -11,15 +11,26 @@
 //   pass k (1..3): tile histogram  ->  exclusive scan  ->  scatter (counting
 //                  sort of a 4096-row tile in LDS, then runs of rows written
 //                  contiguously to their partition)  ->  next segment offsets
-//   join:          one workgroup per (partition, S chunk of 8192 rows): build
-//                  the partition's R rows into an LDS table (8192 slots,
-//                  <= 5120 rows per round), probe the chunk's S rows, count,
-//                  block-scan, reserve the block's output with ONE global
-//                  atomic, and write every pair at its exact position.
+//   join:          one work item per (partition, S chunk): build the
+//                  partition's R rows into an LDS table, probe the chunk's S
+//                  rows, count, block-scan, reserve the block's output with
+//                  ONE global atomic, and write every pair at its position.
+//
+// Partitioned rows are packed: 16-B {key, payload} (64-bit keys) or 8-B
+// (key << 32 | row id) (the reference's i32 types), so a row moves with one
+// global load/store and an i32 row is already its own LDS table entry.
+//
+// Scatter and join are persistent (2 workgroups per CU) and software-
+// pipelined: the next tile / work item is loaded into registers before the
+// current one's LDS phase, so HBM latency hides behind LDS work.
 //
 // The reference's count -> prefix -> probe protocol (join_v1.mlir:288-521) is
 // kept, but per workgroup and on LDS, so the output needs no staging buffer
 // and has no overflow path.
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
+
 #include "hj_internal.h"
 
 namespace hj {
@@ -29,27 +40,49 @@ typedef unsigned long long u64;
 constexpr u64 kGold = 0x9E3779B97F4A7C15ull;
 constexpr int kTile = 4096;        // rows per partition-pass tile
 constexpr int kPassThreads = 512;  // 8 rows per thread
-constexpr int kJoinThreads = 1024;
-constexpr int kJoinItems = 8;      // S rows per thread -> 8192-row chunk
-constexpr int kChunk = kJoinThreads * kJoinItems;
-constexpr int kTSlots = 8192;      // LDS table slots (128 KiB wide)
-constexpr int kRCap = 5120;        // build rows per round (load factor <= 0.625)
+constexpr int kPassRows = kTile / kPassThreads;
+constexpr int kJoinItems = 4;      // S rows per thread per sub-chunk of the join kernel
+constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build serves all)
+constexpr int kPackedRow = 3;      // SrcForm of partition-pass outputs (packed rows)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
 
-// --------------------------------------------------------------- helpers
-// Largest s in [0, nseg) with start[s] <= w (start[nseg] > w): segment of
-// work item / tile w.  Empty segments are skipped automatically.
-__device__ __forceinline__ int find_seg(const unsigned *start, int nseg, unsigned w) {
-    int lo = 0, hi = nseg;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (start[mid] <= w) lo = mid;
-        else hi = mid;
+// --------------------------------------------------------------- rows
+template <bool WIDE>
+struct Row;
+
+template <>
+struct Row<true> {   // 64-bit key / 64-bit payload
+    typedef ulonglong2 T;
+    static __device__ __forceinline__ u64 key(const T &r) { return r.x; }
+    static __device__ __forceinline__ u64 pay(const T &r) { return r.y; }
+    static __device__ __forceinline__ T make(u64 k, u64 p) { return make_ulonglong2(k, p); }
+    static __device__ __forceinline__ T zero() { return make_ulonglong2(0ull, 0ull); }
+};
+
+template <>
+struct Row<false> {   // i32 key (zero-extended) / i32 row id, packed key << 32 | row id
+    typedef u64 T;
+    static __device__ __forceinline__ u64 key(const T &r) { return r >> 32; }
+    static __device__ __forceinline__ u64 pay(const T &r) { return r & 0xffffffffull; }
+    static __device__ __forceinline__ T make(u64 k, u64 p) { return (k << 32) | (p & 0xffffffffull); }
+    static __device__ __forceinline__ T zero() { return 0ull; }
+};
+
+// Row `row` of a pass input in form FORM.
+template <bool WIDE, int FORM>
+__device__ __forceinline__ typename Row<WIDE>::T load_row(const SrcDev &s, long long row) {
+    typedef Row<WIDE> R;
+    if constexpr (FORM == kPackedRow || FORM == kPacked64) {
+        return ((const typename R::T *)s.key)[row];
+    } else if constexpr (FORM == kCol32) {
+        return R::make((u64)(unsigned)((const int *)s.key)[row], (u64)(s.row_base + row));
+    } else {   // kCols64
+        return R::make(((const u64 *)s.key)[row], ((const u64 *)s.pay)[row]);
     }
-    return lo;
 }
 
+// --------------------------------------------------------------- helpers
 // Block-wide exclusive scan of one u64 per thread.  All NT threads must call.
 template <int NT>
 __device__ __forceinline__ u64 block_excl_scan(u64 v, u64 *wsum, u64 *total) {
@@ -79,30 +112,6 @@ __device__ __forceinline__ u64 block_excl_scan(u64 v, u64 *wsum, u64 *total) {
     return before + x - v;
 }
 
-// Row loaders of the partition passes' first input.
-template <class KT, class PT, int FORM>
-__device__ __forceinline__ void load_row(const void *key, const void *pay, long long row_base, long long row, KT &k,
-                                         PT &p) {
-    if constexpr (FORM == kPacked64) {
-        const ulonglong2 v = ((const ulonglong2 *)key)[row];
-        k = (KT)v.x;
-        p = (PT)v.y;
-    } else if constexpr (FORM == kCol32) {
-        k = (KT)(unsigned)((const int *)key)[row];
-        p = (PT)(row_base + row);
-    } else {
-        k = ((const KT *)key)[row];
-        p = ((const PT *)pay)[row];
-    }
-}
-
-template <class KT, int FORM>
-__device__ __forceinline__ KT load_key(const void *key, long long row) {
-    if constexpr (FORM == kPacked64) return (KT)((const u64 *)key)[2 * row];
-    else if constexpr (FORM == kCol32) return (KT)(unsigned)((const int *)key)[row];
-    else return ((const KT *)key)[row];
-}
-
 // --------------------------------------------------------------- maps
 // start[s] = sum over s' < s of count(s'), count(s) = ceil(len_a(s) / chunk),
 // or 0 when off_b is given and segment s of b is empty (no build rows ->
@@ -127,6 +136,15 @@ __global__ __launch_bounds__(1024) void k_chunk_map(const u64 *off_a, const u64 
         run += live ? (len + chunk - 1) / chunk : 0ull;
     }
     if (threadIdx.x == 0) start[nseg] = (unsigned)total;
+}
+
+// item -> segment list from a chunk map (start[] as written by k_chunk_map):
+// one thread per segment writes its items' owner, so consumers need a single
+// load instead of a log2(nseg)-step dependent binary search.
+__global__ __launch_bounds__(256) void k_work_list(const unsigned *start, int nseg, unsigned *owner) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= nseg) return;
+    for (unsigned w = start[s]; w < start[s + 1]; ++w) owner[w] = (unsigned)s;
 }
 
 __global__ void k_set_off(u64 *off, u64 n) {
@@ -183,138 +201,181 @@ __global__ __launch_bounds__(1024) void k_scan_add(u64 *a, u64 n, const u64 *sum
 
 // --------------------------------------------------------------- partition pass
 struct PassArgs {
-    const void *in_key;
-    const void *in_pay;
-    long long row_base;
-    const u64 *seg_off;       // nseg + 1
+    SrcDev in;                   // pass input (key/pay/row_base/form; n unused)
+    const u64 *seg_off;          // nseg + 1
     int nseg;
     const unsigned *tile_start;  // nseg + 1
-    u64 *hist;                // [seg][bin][tile] counts, then exclusive offsets
-    void *out_key;
-    void *out_pay;
-    u64 *next_off;            // nseg * F + 1
-    int shift;                // bin = (hash >> shift) & (F - 1)
+    const unsigned *tile_owner;  // tile -> segment (nseg > 1)
+    u64 *hist;                   // [seg][bin][tile] counts, then exclusive offsets
+    void *out;                   // packed rows
+    u64 *next_off;               // nseg * F + 1
+    int shift;                   // bin = (hash >> shift) & (F - 1)
     int fbits;
 };
 
-__device__ __forceinline__ void tile_of(const PassArgs &a, unsigned wg, int &seg, unsigned &t, unsigned &ntiles,
-                                        u64 &lo, u64 &hi) {
-    seg = a.nseg == 1 ? 0 : find_seg(a.tile_start, a.nseg, wg);
-    t = wg - a.tile_start[seg];
-    ntiles = a.tile_start[seg + 1] - a.tile_start[seg];
-    lo = a.seg_off[seg] + (u64)t * kTile;
-    const u64 e = a.seg_off[seg + 1];
-    hi = lo + kTile < e ? lo + kTile : e;
+struct TileRange {
+    int seg;
+    unsigned t, ntiles;
+    u64 lo, hi;
+};
+
+__device__ __forceinline__ TileRange tile_range(const PassArgs &a, unsigned wg) {
+    TileRange r;
+    r.seg = a.nseg == 1 ? 0 : (int)a.tile_owner[wg];
+    r.t = wg - a.tile_start[r.seg];
+    r.ntiles = a.tile_start[r.seg + 1] - a.tile_start[r.seg];
+    r.lo = a.seg_off[r.seg] + (u64)r.t * kTile;
+    const u64 e = a.seg_off[r.seg + 1];
+    r.hi = r.lo + kTile < e ? r.lo + kTile : e;
+    return r;
 }
 
-template <class KT, int FORM>
+// Per-tile bin counts.  Keys are read 16 B per lane (two keys of a key
+// column, or the key half of one packed row).
+template <bool WIDE, int FORM>
 __global__ __launch_bounds__(kPassThreads) void k_hist(PassArgs a) {
-    __shared__ unsigned cnt[256];
+    typedef Row<WIDE> R;
+    __shared__ unsigned cnt[512];
     const unsigned wg = blockIdx.x;
     if (wg >= a.tile_start[a.nseg]) return;   // upper-bound grid
-    int seg;
-    unsigned t, ntiles;
-    u64 lo, hi;
-    tile_of(a, wg, seg, t, ntiles, lo, hi);
+    const TileRange tr = tile_range(a, wg);
     const unsigned F = 1u << a.fbits;
     for (unsigned b = threadIdx.x; b < F; b += kPassThreads) cnt[b] = 0u;
     __syncthreads();
+    auto bin_of = [&](u64 k) { return (unsigned)(rhash(k) >> a.shift) & (F - 1); };
+    if constexpr (FORM == kCols64) {
+        // two consecutive keys per lane (one 16-B load): rows lo + 2*(i*NT + tid) + {0,1}
+        const bool al = ((((uintptr_t)a.in.key) & 15) == 0) && ((tr.lo & 1) == 0);
 #pragma unroll
-    for (int i = 0; i < kTile / kPassThreads; ++i) {
-        const u64 row = lo + (u64)i * kPassThreads + threadIdx.x;
-        if (row < hi) {
-            const KT k = load_key<KT, FORM>(a.in_key, (long long)row);
-            atomicAdd(&cnt[(unsigned)(rhash((u64)k) >> a.shift) & (F - 1)], 1u);
+        for (int i = 0; i < kPassRows / 2; ++i) {
+            const u64 row = tr.lo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
+            if (al && row + 1 < tr.hi) {
+                const ulonglong2 kk = *(const ulonglong2 *)((const u64 *)a.in.key + row);
+                atomicAdd(&cnt[bin_of(kk.x)], 1u);
+                atomicAdd(&cnt[bin_of(kk.y)], 1u);
+            } else {
+                if (row < tr.hi) atomicAdd(&cnt[bin_of(((const u64 *)a.in.key)[row])], 1u);
+                if (row + 1 < tr.hi) atomicAdd(&cnt[bin_of(((const u64 *)a.in.key)[row + 1])], 1u);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kPassRows; ++i) {
+            const u64 row = tr.lo + (u64)i * kPassThreads + threadIdx.x;
+            if (row < tr.hi) atomicAdd(&cnt[bin_of(R::key(load_row<WIDE, FORM>(a.in, (long long)row)))], 1u);
         }
     }
     __syncthreads();
-    const u64 base = (u64)a.tile_start[seg] * F;
-    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) a.hist[base + (u64)b * ntiles + t] = cnt[b];
+    const u64 base = (u64)a.tile_start[tr.seg] * F;
+    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) a.hist[base + (u64)b * tr.ntiles + tr.t] = cnt[b];
 }
 
-template <class KT, class PT, int FORM>
-__global__ __launch_bounds__(kPassThreads) void k_scatter(PassArgs a) {
-    constexpr int IT = kTile / kPassThreads;
-    __shared__ KT sk[kTile];
-    __shared__ PT sp[kTile];
-    __shared__ unsigned char sb[kTile];
-    __shared__ unsigned cnt[256];
-    __shared__ long long dst_base[256];
-    const unsigned wg = blockIdx.x;
-    if (wg >= a.tile_start[a.nseg]) return;
-    int seg;
-    unsigned t, ntiles;
-    u64 lo, hi;
-    tile_of(a, wg, seg, t, ntiles, lo, hi);
+// Counting sort of each tile by bin in LDS, then contiguous runs written to
+// the bins' scanned output offsets.  Persistent: a workgroup walks tiles
+// wg, wg + grid, ... and loads the next tile's rows before sorting this one.
+template <bool WIDE, int FORM>
+__global__ __launch_bounds__(kPassThreads, 4) void k_scatter(PassArgs a) {   // 2 workgroups per CU: <= 128 VGPRs
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    constexpr int IT = kPassRows;
+    __shared__ T stage[kTile];
+    __shared__ unsigned short sb[kTile];
+    __shared__ unsigned cnt[512];
+    __shared__ long long dst_base[512];
+    const unsigned total = a.tile_start[a.nseg];
+    unsigned wg = blockIdx.x;
+    if (wg >= total) return;
     const unsigned F = 1u << a.fbits;
-    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) cnt[b] = 0u;
-    __syncthreads();
-    KT k[IT];
-    PT p[IT];
-    unsigned bin[IT], rank[IT];
+    T *out = (T *)a.out;
+
+    TileRange tr = tile_range(a, wg);
+    T row[IT];
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-        const u64 row = lo + (u64)i * kPassThreads + threadIdx.x;
-        if (row < hi) {
-            load_row<KT, PT, FORM>(a.in_key, a.in_pay, a.row_base, (long long)row, k[i], p[i]);
-            bin[i] = (unsigned)(rhash((u64)k[i]) >> a.shift) & (F - 1);
-            rank[i] = atomicAdd(&cnt[bin[i]], 1u);
-        } else {
-            bin[i] = 0xFFFFFFFFu;
-        }
+        const u64 r = tr.lo + (u64)i * kPassThreads + threadIdx.x;
+        row[i] = r < tr.hi ? load_row<WIDE, FORM>(a.in, (long long)r) : R::zero();
     }
-    __syncthreads();
-    // exclusive scan of the F bin counts (first wave, 4 bins per lane) and
-    // the destination base of each bin's run: scanned global offset - local start
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        unsigned c[4], s = 0;
+    while (true) {
+        // prefetch the next tile
+        const unsigned wn = wg + gridDim.x;
+        const bool more = wn < total;
+        TileRange tn;
+        T nrow[IT];
+        if (more) {
+            tn = tile_range(a, wn);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned b = lane * 4 + j;
-            c[j] = b < F ? cnt[b] : 0u;
-            s += c[j];
-        }
-        unsigned x = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        unsigned run = x - s;
-        const u64 hb = (u64)a.tile_start[seg] * F;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned b = lane * 4 + j;
-            if (b < F) {
-                cnt[b] = run;   // now the local start of bin b
-                dst_base[b] = (long long)a.hist[hb + (u64)b * ntiles + t] - (long long)run;
+            for (int i = 0; i < IT; ++i) {
+                const u64 r = tn.lo + (u64)i * kPassThreads + threadIdx.x;
+                nrow[i] = r < tn.hi ? load_row<WIDE, FORM>(a.in, (long long)r) : R::zero();
             }
-            run += c[j];
         }
-    }
-    __syncthreads();
+        // ---- sort this tile
+        for (unsigned b = threadIdx.x; b < F; b += kPassThreads) cnt[b] = 0u;
+        __syncthreads();
+        unsigned br[IT];   // bin << 16 | rank within the tile's bin (bin < 512, rank < 4096)
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-        if (bin[i] != 0xFFFFFFFFu) {
-            const unsigned pos = cnt[bin[i]] + rank[i];
-            sk[pos] = k[i];
-            sp[pos] = p[i];
-            sb[pos] = (unsigned char)bin[i];
+        for (int i = 0; i < IT; ++i) {
+            const u64 r = tr.lo + (u64)i * kPassThreads + threadIdx.x;
+            if (r < tr.hi) {
+                const unsigned b = (unsigned)(rhash(R::key(row[i])) >> a.shift) & (F - 1);
+                br[i] = (b << 16) | atomicAdd(&cnt[b], 1u);
+            } else {
+                br[i] = 0xFFFFFFFFu;
+            }
         }
-    }
-    __syncthreads();
-    const unsigned n = (unsigned)(hi - lo);
-    KT *ok = (KT *)a.out_key;
-    PT *op = (PT *)a.out_pay;
+        __syncthreads();
+        // exclusive scan of the bin counts (first wave, 8 bins per lane) and each
+        // bin's run destination base = scanned global offset - local start
+        if (threadIdx.x < 64) {
+            const int lane = threadIdx.x;
+            unsigned c[8], s = 0;
 #pragma unroll
-    for (int i = 0; i < IT; ++i) {
-        const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
-        if (j < n) {
-            const u64 dst = (u64)(dst_base[sb[j]] + (long long)j);
-            ok[dst] = sk[j];
-            op[dst] = sp[j];
+            for (int j = 0; j < 8; ++j) {
+                const unsigned b = lane * 8 + j;
+                c[j] = b < F ? cnt[b] : 0u;
+                s += c[j];
+            }
+            unsigned x = s;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            unsigned run = x - s;
+            const u64 hb = (u64)a.tile_start[tr.seg] * F;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const unsigned b = lane * 8 + j;
+                if (b < F) {
+                    cnt[b] = run;
+                    dst_base[b] = (long long)a.hist[hb + (u64)b * tr.ntiles + tr.t] - (long long)run;
+                }
+                run += c[j];
+            }
         }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            if (br[i] != 0xFFFFFFFFu) {
+                const unsigned b = br[i] >> 16;
+                const unsigned pos = cnt[b] + (br[i] & 0xffffu);
+                stage[pos] = row[i];
+                sb[pos] = (unsigned short)b;
+            }
+        }
+        __syncthreads();
+        const unsigned n = (unsigned)(tr.hi - tr.lo);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
+            if (j < n) out[(u64)(dst_base[sb[j]] + (long long)j)] = stage[j];
+        }
+        if (!more) break;
+        __syncthreads();   // stage/cnt reused by the next tile
+        wg = wn;
+        tr = tn;
+#pragma unroll
+        for (int i = 0; i < IT; ++i) row[i] = nrow[i];
     }
 }
 
@@ -333,204 +394,331 @@ __global__ __launch_bounds__(256) void k_next_off(PassArgs a) {
 
 // --------------------------------------------------------------- join
 struct JoinArgs {
-    const void *rk, *rp, *sk, *sp;   // partitioned SoA relations
+    const void *r, *s;               // partitioned packed rows
     const u64 *r_off, *s_off;        // P + 1 each
     int P;
     const unsigned *work_start;      // P + 1: S chunks per partition (0 if no R rows)
-    int tshift;                      // LDS slot = (hash >> tshift) & (kTSlots - 1)
+    const unsigned *work_owner;      // work item -> partition
+    int tshift;                      // LDS slot = (hash >> tshift) & (slots - 1)
     void *out_r, *out_s;
     long long cap;
     u64 *counter;
     u64 *dup_flag;                   // set to 1 if any partition's build rows repeat a key
 };
 
-struct JWide {
-    typedef u64 KT;
-    typedef u64 PT;
-    static constexpr bool kNullKeys = true;
-};
-struct JNarrow {
-    typedef unsigned KT;
-    typedef unsigned PT;
-    static constexpr bool kNullKeys = false;
+struct Item {
+    u64 s_lo, s_hi, r_lo, r_hi;
 };
 
-template <class J, bool WRITE>
-__global__ __launch_bounds__(kJoinThreads) void k_join(JoinArgs a) {
-    typedef typename J::KT KT;
-    typedef typename J::PT PT;
-    constexpr u64 kEmpty = J::kNullKeys ? kEmptyKey64 : ~0ull;
-    constexpr unsigned kMask = kTSlots - 1;
-    // wide: tkey/tpay; narrow: tkey holds packed (key << 32 | row id)
-    __shared__ u64 tkey[kTSlots];
-    __shared__ PT tpay[J::kNullKeys ? kTSlots : 1];
+template <int CH>
+__device__ __forceinline__ Item item_of(const JoinArgs &a, unsigned w) {
+    const int p = (int)a.work_owner[w];
+    const unsigned c = w - a.work_start[p];
+    Item it;
+    it.s_lo = a.s_off[p] + (u64)c * CH;
+    const u64 e = a.s_off[p + 1];
+    it.s_hi = it.s_lo + CH < e ? it.s_lo + CH : e;
+    it.r_lo = a.r_off[p];
+    it.r_hi = a.r_off[p + 1];
+    return it;
+}
+
+// A persistent workgroup of NT threads walks work items w = wg, wg + grid, ...
+// Work item = (partition, S chunk of up to kJoinSub * NT * SI rows): build
+// the partition's R rows into a 2^TSL-slot LDS table (rounds of RCAP rows
+// for oversized partitions), then probe the chunk in sub-chunks of NT * SI
+// rows.  The next item's first S sub-chunk and R round are loaded into
+// registers before this item's LDS phase.
+// ABL (diagnostics only, micro/join_micro.hip; the product uses 0) switches
+// phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build.
+template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0>
+__global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per SIMD: <= 128 VGPRs
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // output element
+    constexpr int TS = 1 << TSL;
+    constexpr unsigned kMask = TS - 1;
+    constexpr int SI = kJoinItems;            // S rows per thread per sub-chunk
+    constexpr int RCAP = TS * 5 / 8;          // build rows per round (load factor <= 0.625)
+    constexpr int RI = RCAP / NT;             // build rows per thread per round
+    constexpr int SUBR = NT * SI;             // rows per sub-chunk
+    constexpr int CH = kJoinSub * SUBR;       // rows per work item
+    // wide: EMPTY key INT64_MIN (rows with that key take the null path);
+    // narrow: the all-ones word (row ids < 2^31 never produce it)
+    constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
+    __shared__ u64 tkey[TS];                  // wide: keys; narrow: packed rows
+    __shared__ u64 tpay[WIDE ? TS : 1];
     __shared__ u64 wsum[16];
     __shared__ u64 s_base;
     __shared__ unsigned s_dup;
 
-    const unsigned w = blockIdx.x;
-    if (w >= a.work_start[a.P]) return;   // upper-bound grid
-    const int p = find_seg(a.work_start, a.P, w);
-    const unsigned c = w - a.work_start[p];
-    const u64 s_lo = a.s_off[p] + (u64)c * kChunk;
-    const u64 s_end = a.s_off[p + 1];
-    const u64 s_hi = s_lo + kChunk < s_end ? s_lo + kChunk : s_end;
-    const u64 r_lo = a.r_off[p], r_hi = a.r_off[p + 1];
+    const unsigned total = a.work_start[a.P];
+    unsigned w = blockIdx.x;
+    if (w >= total) return;
+    const T *rrows = (const T *)a.r;
+    const T *srows = (const T *)a.s;
+    PT *orr = (PT *)a.out_r;
+    PT *oss = (PT *)a.out_s;
 
-    KT k[kJoinItems];
-    PT pv[kJoinItems];
-    unsigned h0[kJoinItems];
-    bool v[kJoinItems];
-    bool has_null_s = false;
+    Item it = item_of<CH>(a, w);
+    T sv_[SI], rv_[RI];
 #pragma unroll
-    for (int i = 0; i < kJoinItems; ++i) {
-        const u64 row = s_lo + (u64)i * kJoinThreads + threadIdx.x;
-        v[i] = row < s_hi;
-        k[i] = v[i] ? ((const KT *)a.sk)[row] : (KT)0;
-        pv[i] = v[i] ? ((const PT *)a.sp)[row] : (PT)0;
-        h0[i] = (unsigned)(rhash((u64)k[i]) >> a.tshift) & kMask;
-        if (J::kNullKeys && v[i] && (u64)k[i] == kEmptyKey64) {
-            has_null_s = true;
-            v[i] = false;   // matched by the null pass below
-        }
+    for (int i = 0; i < SI; ++i) {
+        const u64 row = it.s_lo + (u64)i * NT + threadIdx.x;
+        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
     }
-    u64 n_null_r = 0;
-    const KT *rk = (const KT *)a.rk;
-    const PT *rp = (const PT *)a.rp;
-
-    for (u64 r0 = r_lo; r0 < r_hi; r0 += kRCap) {
-        const u64 r1 = r0 + kRCap < r_hi ? r0 + kRCap : r_hi;
-        // ---- init: every slot EMPTY (16-B LDS stores)
-        for (int j = threadIdx.x; j < kTSlots / 2; j += kJoinThreads)
-            ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
-        if (threadIdx.x == 0) s_dup = 0u;
-        __syncthreads();
-        // ---- build this round's rows
-        bool dup = false;
-        for (u64 row = r0 + threadIdx.x; row < r1; row += kJoinThreads) {
-            const KT key = rk[row];
-            const PT pay = rp[row];
-            if (J::kNullKeys && (u64)key == kEmptyKey64) {
-                ++n_null_r;
-                continue;
-            }
-            unsigned h = (unsigned)(rhash((u64)key) >> a.tshift) & kMask;
-            const u64 val = J::kNullKeys ? (u64)key : (((u64)key << 32) | (u64)pay);
-            while (true) {
-                const u64 old = atomicCAS(&tkey[h], kEmpty, val);
-                if (old == kEmpty) break;
-                dup |= J::kNullKeys ? (old == (u64)key) : ((old >> 32) == (u64)key);
-                h = (h + 1) & kMask;
-            }
-            if constexpr (J::kNullKeys) tpay[h] = pay;
-        }
-        if (dup) s_dup = 1u;
-        __syncthreads();
-        const bool unique = s_dup == 0u;
-        if (!unique && threadIdx.x == 0)
-            __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // ---- count (and remember the matched slot when build keys are unique)
-        unsigned m[kJoinItems];
-        u64 cnt = 0;
 #pragma unroll
-        for (int i = 0; i < kJoinItems; ++i) {
-            m[i] = 0xFFFFFFFFu;
-            if (!v[i]) continue;
-            unsigned h = h0[i];
-            while (true) {
-                const u64 sv = tkey[h];
-                if (sv == kEmpty) break;
-                const bool hit = J::kNullKeys ? (sv == (u64)k[i]) : ((sv >> 32) == (u64)k[i]);
-                if (hit) {
-                    ++cnt;
-                    if (unique) {
-                        m[i] = h;
-                        break;
+    for (int i = 0; i < RI; ++i) {
+        const u64 row = it.r_lo + (u64)i * NT + threadIdx.x;
+        rv_[i] = row < it.r_hi ? rrows[row] : R::zero();
+    }
+
+    while (true) {
+        // ---- prefetch the next work item
+        const unsigned wn = w + gridDim.x;
+        const bool more = wn < total;
+        Item nx;
+        T nsv[SI], nrv[RI];
+        if (more) {
+            nx = item_of<CH>(a, wn);
+#pragma unroll
+            for (int i = 0; i < SI; ++i) {
+                const u64 row = nx.s_lo + (u64)i * NT + threadIdx.x;
+                nsv[i] = row < nx.s_hi ? srows[row] : R::zero();
+            }
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const u64 row = nx.r_lo + (u64)i * NT + threadIdx.x;
+                nrv[i] = row < nx.r_hi ? rrows[row] : R::zero();
+            }
+        }
+
+        u64 n_null_r = 0;
+        bool any_null_s = false;
+        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += RCAP) {
+            const u64 r1 = r0 + RCAP < it.r_hi ? r0 + RCAP : it.r_hi;
+            if (r0 != it.r_lo) {   // later rounds (oversized partitions)
+#pragma unroll
+                for (int i = 0; i < RI; ++i) {
+                    const u64 row = r0 + (u64)i * NT + threadIdx.x;
+                    rv_[i] = row < r1 ? rrows[row] : R::zero();
+                }
+            }
+            // ---- init: every slot EMPTY (16-B LDS stores)
+            for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
+            if (threadIdx.x == 0) s_dup = 0u;
+            __syncthreads();
+            // ---- build this round's rows: every row's first CAS is issued
+            // before any result is used (RI independent LDS atomics in flight)
+            bool dup = false;
+            unsigned hb[RI];
+            u64 ob[RI], vb[RI];
+            bool act[RI];
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const u64 row = r0 + (u64)i * NT + threadIdx.x;
+                const u64 key = R::key(rv_[i]);
+                act[i] = row < r1;
+                if (WIDE && act[i] && key == kEmptyKey64) {
+                    ++n_null_r;
+                    act[i] = false;
+                }
+                if constexpr ((ABL & 8) != 0) act[i] = false;
+                hb[i] = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                if constexpr (WIDE) vb[i] = key;
+                else vb[i] = rv_[i];
+                ob[i] = act[i] ? atomicCAS(&tkey[hb[i]], kEmpty, vb[i]) : kEmpty;
+            }
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                if (!act[i]) continue;
+                const u64 key = R::key(rv_[i]);
+                unsigned h = hb[i];
+                u64 old = ob[i];
+                while (old != kEmpty) {
+                    dup |= WIDE ? (old == key) : ((old >> 32) == key);
+                    h = (h + 1) & kMask;
+                    old = atomicCAS(&tkey[h], kEmpty, vb[i]);
+                }
+                if constexpr (WIDE) tpay[h] = R::pay(rv_[i]);
+            }
+            if (dup) s_dup = 1u;
+            __syncthreads();
+            const bool unique = s_dup == 0u;
+            if (!unique && threadIdx.x == 0)
+                __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+            // ---- probe the chunk, one sub-chunk of S rows at a time
+            for (u64 sb = it.s_lo; sb < it.s_hi; sb += SUBR) {
+                if (sb != it.s_lo || r0 != it.r_lo) {
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 row = sb + (u64)i * NT + threadIdx.x;
+                        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
                     }
                 }
-                h = (h + 1) & kMask;
-            }
-        }
-        u64 total;
-        const u64 pre = block_excl_scan<kJoinThreads>(cnt, wsum, &total);
-        if constexpr (!WRITE) {
-            if (threadIdx.x == 0 && total) atomicAdd(a.counter, total);
-        } else if (total) {
-            if (threadIdx.x == 0) s_base = atomicAdd(a.counter, total);
-            __syncthreads();
-            u64 pos = s_base + pre;
-            PT *orr = (PT *)a.out_r;
-            PT *oss = (PT *)a.out_s;
+                // first slot of every row read before any is resolved (SI
+                // independent LDS reads in flight); most rows end there
+                unsigned m[SI], hp[SI];
+                u64 e0[SI];
+                bool pa[SI];
+                u64 cnt = 0;
 #pragma unroll
-            for (int i = 0; i < kJoinItems; ++i) {
-                if (!v[i]) continue;
-                if (unique) {
-                    if (m[i] != 0xFFFFFFFFu) {
-                        if (pos < (u64)a.cap) {
-                            orr[pos] = J::kNullKeys ? tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull);
-                            oss[pos] = pv[i];
-                        }
-                        ++pos;
+                for (int i = 0; i < SI; ++i) {
+                    m[i] = 0xFFFFFFFFu;
+                    const u64 row = sb + (u64)i * NT + threadIdx.x;
+                    const u64 key = R::key(sv_[i]);
+                    pa[i] = row < it.s_hi;
+                    if (WIDE && pa[i] && key == kEmptyKey64) {   // matched by the null pass below
+                        any_null_s = true;
+                        pa[i] = false;
                     }
-                } else {
-                    unsigned h = h0[i];
-                    while (true) {
-                        const u64 sv = tkey[h];
-                        if (sv == kEmpty) break;
-                        const bool hit = J::kNullKeys ? (sv == (u64)k[i]) : ((sv >> 32) == (u64)k[i]);
-                        if (hit) {
-                            if (pos < (u64)a.cap) {
-                                orr[pos] = J::kNullKeys ? tpay[h] : (PT)(sv & 0xffffffffull);
-                                oss[pos] = pv[i];
+                    if constexpr ((ABL & 4) != 0) {
+                        cnt += pa[i] ? (key & 1) : 0;
+                        pa[i] = false;
+                    }
+                    hp[i] = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                    e0[i] = pa[i] ? tkey[hp[i]] : kEmpty;
+                }
+#pragma unroll
+                for (int i = 0; i < SI; ++i) {
+                    if (!pa[i]) continue;
+                    const u64 key = R::key(sv_[i]);
+                    unsigned h = hp[i];
+                    u64 e = e0[i];
+                    while (e != kEmpty) {
+                        if ((WIDE ? e : (e >> 32)) == key) {
+                            ++cnt;
+                            if (unique) {
+                                m[i] = h;
+                                break;
                             }
-                            ++pos;
                         }
                         h = (h + 1) & kMask;
+                        e = tkey[h];
                     }
                 }
-            }
-        }
-        __syncthreads();   // table reused by the next round
-    }
-
-    // ---- INT64_MIN keys (the wide EMPTY sentinel): matched outside the table.
-    if constexpr (J::kNullKeys) {
-        if (__syncthreads_or(has_null_s ? 1 : 0)) {
-            u64 nn;
-            (void)block_excl_scan<kJoinThreads>(n_null_r, wsum, &nn);   // null R rows of this partition
-            u64 cnt = 0;
-            if (has_null_s) {
+                u64 tot;
+                const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
+                if constexpr (!WRITE) {
+                    if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                } else if (tot) {
+                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * CH : atomicAdd(a.counter, tot);
+                    __syncthreads();
+                    u64 pos = s_base + pre;
 #pragma unroll
-                for (int i = 0; i < kJoinItems; ++i) {
-                    const u64 row = s_lo + (u64)i * kJoinThreads + threadIdx.x;
-                    if (row < s_hi && (u64)k[i] == kEmptyKey64) cnt += nn;
-                }
-            }
-            u64 total;
-            const u64 pre = block_excl_scan<kJoinThreads>(cnt, wsum, &total);
-            if constexpr (!WRITE) {
-                if (threadIdx.x == 0 && total) atomicAdd(a.counter, total);
-            } else if (total) {
-                if (threadIdx.x == 0) s_base = atomicAdd(a.counter, total);
-                __syncthreads();
-                u64 pos = s_base + pre;
-                if (has_null_s) {
-                    for (int i = 0; i < kJoinItems; ++i) {
-                        const u64 row = s_lo + (u64)i * kJoinThreads + threadIdx.x;
-                        if (!(row < s_hi && (u64)k[i] == kEmptyKey64)) continue;
-                        for (u64 r = r_lo; r < r_hi; ++r) {
-                            if ((u64)rk[r] != kEmptyKey64) continue;
-                            if (pos < (u64)a.cap) {
-                                ((PT *)a.out_r)[pos] = rp[r];
-                                ((PT *)a.out_s)[pos] = pv[i];
+                    for (int i = 0; i < SI; ++i) {
+                        if constexpr ((ABL & 2) != 0) break;
+                        const PT spay = (PT)R::pay(sv_[i]);
+                        if (unique) {
+                            if (m[i] != 0xFFFFFFFFu) {
+                                if (pos < (u64)a.cap) {
+                                    orr[pos] = WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull);
+                                    oss[pos] = spay;
+                                }
+                                ++pos;
                             }
-                            ++pos;
+                        } else {
+                            const u64 row = sb + (u64)i * NT + threadIdx.x;
+                            const u64 key = R::key(sv_[i]);
+                            if (row >= it.s_hi || (WIDE && key == kEmptyKey64)) continue;
+                            unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                            while (true) {
+                                const u64 e = tkey[h];
+                                if (e == kEmpty) break;
+                                if ((WIDE ? e : (e >> 32)) == key) {
+                                    if (pos < (u64)a.cap) {
+                                        orr[pos] = WIDE ? (PT)tpay[h] : (PT)(e & 0xffffffffull);
+                                        oss[pos] = spay;
+                                    }
+                                    ++pos;
+                                }
+                                h = (h + 1) & kMask;
+                            }
                         }
                     }
+                    __syncthreads();   // s_base reused by the next sub-chunk
+                }
+            }
+            __syncthreads();   // table reused by the next round / item
+        }
+
+        // ---- INT64_MIN keys (the wide EMPTY sentinel): matched outside the table
+        if constexpr (WIDE) {
+            if (__syncthreads_or(any_null_s ? 1 : 0)) {
+                u64 nn;
+                (void)block_excl_scan<NT>(n_null_r, wsum, &nn);   // null R rows of this partition
+                for (u64 sb = it.s_lo; sb < it.s_hi; sb += SUBR) {
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 row = sb + (u64)i * NT + threadIdx.x;
+                        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
+                    }
+                    u64 cnt = 0;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 row = sb + (u64)i * NT + threadIdx.x;
+                        if (row < it.s_hi && R::key(sv_[i]) == kEmptyKey64) cnt += nn;
+                    }
+                    u64 tot;
+                    const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
+                    if constexpr (!WRITE) {
+                        if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                    } else if (tot) {
+                        if (threadIdx.x == 0) s_base = atomicAdd(a.counter, tot);
+                        __syncthreads();
+                        u64 pos = s_base + pre;
+                        for (int i = 0; i < SI; ++i) {
+                            const u64 row = sb + (u64)i * NT + threadIdx.x;
+                            if (!(row < it.s_hi && R::key(sv_[i]) == kEmptyKey64)) continue;
+                            for (u64 r = it.r_lo; r < it.r_hi; ++r) {
+                                const T rr = rrows[r];
+                                if (R::key(rr) != kEmptyKey64) continue;
+                                if (pos < (u64)a.cap) {
+                                    orr[pos] = (PT)R::pay(rr);
+                                    oss[pos] = (PT)R::pay(sv_[i]);
+                                }
+                                ++pos;
+                            }
+                        }
+                        __syncthreads();
+                    }
                 }
             }
         }
+
+        if (!more) break;
+        w = wn;
+        it = nx;
+#pragma unroll
+        for (int i = 0; i < SI; ++i) sv_[i] = nsv[i];
+#pragma unroll
+        for (int i = 0; i < RI; ++i) rv_[i] = nrv[i];
     }
+}
+
+// Join kernel variant: log2 LDS slots and workgroup size.  HJ_JOIN_TSL
+// (11 | 12 | 13) overrides the default for experiments.
+struct JoinVariant {
+    int tsl;
+    int nt;
+};
+JoinVariant join_variant() {
+    static int tsl = [] {
+        const char *e = getenv("HJ_JOIN_TSL");
+        const int v = e ? atoi(e) : 12;
+        return (v == 11 || v == 12 || v == 13) ? v : 12;
+    }();
+    return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256)};
+}
+
+int cu_count() {
+    static int n = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return cus > 0 ? cus : 256;
+    }();
+    return n;
 }
 
 inline unsigned blocks_for(u64 n, u64 per) { return (unsigned)((n + per - 1) / per); }
@@ -539,12 +727,14 @@ inline unsigned blocks_for(u64 n, u64 per) { return (unsigned)((n + per - 1) / p
 
 // ----------------------------------------------------------------- planning
 RadixPlan radix_plan(long long n_build, int force_bits) {
+    // average build rows per partition <= half the join kernel's LDS slots
+    const int tsl = join_variant().tsl;
     RadixPlan pl;
     int bits = 1;
-    while (bits < 24 && ((unsigned long long)n_build >> bits) > 4096ull) ++bits;   // avg build rows per partition <= 4096
+    while (bits < 24 && ((unsigned long long)n_build >> bits) > (1ull << (tsl - 1))) ++bits;
     if (force_bits > 0) bits = force_bits < 24 ? force_bits : 24;
     pl.total_bits = bits;
-    pl.passes = bits <= 8 ? 1 : (bits <= 16 ? 2 : 3);
+    pl.passes = (bits + 8) / 9;   // <= 9 bits (512-way fan-out) per pass
     int left = bits;
     for (int i = 0; i < pl.passes; ++i) {
         pl.bits[i] = (left + (pl.passes - i) - 1) / (pl.passes - i);
@@ -555,49 +745,44 @@ RadixPlan radix_plan(long long n_build, int force_bits) {
 }
 
 size_t radix_hist_elems(long long n, int max_nseg) {
-    return ((size_t)n / kTile + (size_t)max_nseg + 2) * 256;
+    return ((size_t)n / kTile + (size_t)max_nseg + 2) * 512;
 }
 
-int radix_chunk_rows() { return kChunk; }
+int radix_chunk_rows() { return join_variant().nt * kJoinItems * kJoinSub; }
 
-// Partition one relation into the plan's 2^total_bits partitions.
-// Output: out_key/out_pay (SoA, element size esz each) grouped by partition,
-// out_off (P + 1 offsets).  Uses ws.tmp_* as the ping buffer for multi-pass
-// plans.  Asynchronous; no allocation.
-hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out_key,
-                           void *out_pay, unsigned long long *out_off, hipStream_t st) {
+// Partition one relation into the plan's 2^total_bits partitions of packed
+// rows (16 B wide, 8 B narrow) in `out`, with partition offsets in out_off
+// (P + 1).  ws.tmp is the ping buffer of multi-pass plans.  Asynchronous; no
+// allocation.
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out,
+                           unsigned long long *out_off, hipStream_t st) {
     const u64 n = (u64)src.n;
     hipLaunchKernelGGL(k_set_off, dim3(1), dim3(64), 0, st, ws.off_a, n);
     int nseg = 1;
     int shift = 64;
-    const void *in_k = src.key, *in_p = src.pay;
-    int form = src.form;
+    SrcDev in = src;
     u64 *seg_off = ws.off_a;
+    static const unsigned persist_env = [] {
+        const char *e = getenv("HJ_SCATTER_WG_PER_CU");   // experiments: 0 = one tile per workgroup
+        return e ? (unsigned)atoi(e) : 2u;
+    }();
+    const unsigned persist = persist_env ? persist_env * (unsigned)cu_count() : 0xFFFFFFFFu;
     for (int pass = 0; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
         shift -= fb;
         const bool last = pass == pl.passes - 1;
-        // destination of this pass: final buffers on the last pass, else ping/pong
-        void *dk, *dp;
-        if (last) {
-            dk = out_key;
-            dp = out_pay;
-        } else {
-            const bool to_tmp = ((pl.passes - 1 - pass) % 2) == 1;
-            dk = to_tmp ? ws.tmp_key : out_key;
-            dp = to_tmp ? ws.tmp_pay : out_pay;
-        }
+        // destination: final buffer on the last pass, else alternate so the
+        // last pass lands in `out`
+        void *dst = last ? out : ((((pl.passes - 1 - pass) % 2) == 1) ? ws.tmp : out);
         u64 *next_off = last ? out_off : (seg_off == ws.off_a ? ws.off_b : ws.off_a);
         PassArgs a;
-        a.in_key = in_k;
-        a.in_pay = in_p;
-        a.row_base = src.row_base;
+        a.in = in;
         a.seg_off = seg_off;
         a.nseg = nseg;
         a.tile_start = ws.tile_start;
+        a.tile_owner = ws.tile_owner;
         a.hist = ws.hist;
-        a.out_key = dk;
-        a.out_pay = dp;
+        a.out = dst;
         a.next_off = next_off;
         a.shift = shift;
         a.fbits = fb;
@@ -605,76 +790,92 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         hipLaunchKernelGGL(k_chunk_map, dim3(1), dim3(1024), 0, st, (const u64 *)seg_off, (const u64 *)nullptr, nseg,
                            (unsigned)kTile, ws.tile_start);
         const unsigned grid = (unsigned)(n / kTile + nseg + 1);
+        if (nseg > 1)
+            hipLaunchKernelGGL(k_work_list, dim3(blocks_for((u64)nseg, 256)), dim3(256), 0, st,
+                               (const unsigned *)ws.tile_start, nseg, ws.tile_owner);
         const u64 hlen = (u64)grid * F;
         hipError_t e = hipMemsetAsync(ws.hist, 0, hlen * sizeof(u64), st);
         if (e != hipSuccess) return e;
-#define HJ_HIST(KT, FORM) hipLaunchKernelGGL((k_hist<KT, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
-#define HJ_SCAT(KT, PT, FORM) hipLaunchKernelGGL((k_scatter<KT, PT, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
+        const unsigned sgrid = grid < persist ? grid : persist;
+#define HJ_PASS(W, FORM)                                                                                  \
+    do {                                                                                                  \
+        hipLaunchKernelGGL((k_hist<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a);                  \
+        const unsigned nb = blocks_for(hlen, kScanBlock);                                                 \
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, ws.hist, hlen, ws.scan_sums);      \
+        if (nb > 1) {                                                                                     \
+            hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, ws.scan_sums, nb);                \
+            hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, ws.hist, hlen,                    \
+                               (const u64 *)ws.scan_sums);                                                \
+        }                                                                                                 \
+        hipLaunchKernelGGL((k_scatter<W, FORM>), dim3(sgrid), dim3(kPassThreads), 0, st, a);              \
+    } while (0)
         if (wide) {
-            if (form == kPacked64) HJ_HIST(u64, kPacked64);
-            else HJ_HIST(u64, kCols64);
+            if (in.form == kCols64) HJ_PASS(true, kCols64);
+            else HJ_PASS(true, kPackedRow);   // kPacked64 input == packed row layout
         } else {
-            if (form == kCol32) HJ_HIST(unsigned, kCol32);
-            else HJ_HIST(unsigned, kCols64);
+            if (in.form == kCol32) HJ_PASS(false, kCol32);
+            else HJ_PASS(false, kPackedRow);
         }
-        // exclusive scan of the [seg][bin][tile] counts -> output offsets
-        const unsigned nb = blocks_for(hlen, kScanBlock);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, ws.hist, hlen, ws.scan_sums);
-        if (nb > 1) {
-            hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, ws.scan_sums, nb);
-            hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, ws.hist, hlen, (const u64 *)ws.scan_sums);
-        }
-        if (wide) {
-            if (form == kPacked64) HJ_SCAT(u64, u64, kPacked64);
-            else HJ_SCAT(u64, u64, kCols64);
-        } else {
-            if (form == kCol32) HJ_SCAT(unsigned, unsigned, kCol32);
-            else HJ_SCAT(unsigned, unsigned, kCols64);
-        }
-#undef HJ_HIST
-#undef HJ_SCAT
+#undef HJ_PASS
         hipLaunchKernelGGL(k_next_off, dim3(blocks_for((u64)nseg * F + 1, 256)), dim3(256), 0, st, a);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        // next pass reads what this one wrote, as SoA
-        in_k = dk;
-        in_p = dp;
-        form = kCols64;
+        // the next pass reads this pass's packed rows
+        in.key = dst;
+        in.pay = nullptr;
+        in.form = kPackedRow;
         seg_off = next_off;
         nseg *= (int)F;
     }
     return hipSuccess;
 }
 
-hipError_t radix_join(bool wide, const RadixPlan &pl, const void *rk, const void *rp, const unsigned long long *r_off,
-                      const void *sk, const void *sp, const unsigned long long *s_off, long long n_s,
-                      unsigned *work_start, void *out_r, void *out_s, long long cap, unsigned long long *counter,
+hipError_t radix_join(bool wide, const RadixPlan &pl, const void *r_rows, const unsigned long long *r_off,
+                      const void *s_rows, const unsigned long long *s_off, long long n_s, unsigned *work_start,
+                      void *out_r, void *out_s, long long cap, unsigned long long *counter,
                       unsigned long long *dup_flag, bool count_only, hipStream_t st) {
     const int P = 1 << pl.total_bits;
-    hipLaunchKernelGGL(k_chunk_map, dim3(1), dim3(1024), 0, st, s_off, r_off, P, (unsigned)kChunk, work_start);
+    unsigned *work_owner = work_start + P + 1;
+    const JoinVariant jv = join_variant();
+    const unsigned chunk = (unsigned)(jv.nt * kJoinItems * kJoinSub);
+    hipLaunchKernelGGL(k_chunk_map, dim3(1), dim3(1024), 0, st, s_off, r_off, P, chunk, work_start);
+    hipLaunchKernelGGL(k_work_list, dim3(blocks_for((u64)P, 256)), dim3(256), 0, st, (const unsigned *)work_start, P,
+                       work_owner);
     JoinArgs a;
-    a.rk = rk;
-    a.rp = rp;
-    a.sk = sk;
-    a.sp = sp;
+    a.r = r_rows;
+    a.s = s_rows;
     a.r_off = r_off;
     a.s_off = s_off;
     a.P = P;
     a.work_start = work_start;
-    a.tshift = 64 - pl.total_bits - 13;   // 13 = log2(kTSlots): the bits right below the partition bits
+    a.work_owner = work_owner;
+    a.tshift = 64 - pl.total_bits - jv.tsl;   // the hash bits right below the partition bits
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;
     a.counter = counter;
     a.dup_flag = dup_flag;
-    const unsigned grid = (unsigned)((u64)n_s / kChunk + (u64)P + 1);
+    const unsigned items = (unsigned)((u64)n_s / chunk + (u64)P + 1);
+    // persistent grid: as many workgroups as fit at once (LDS-limited)
+    const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
+    const unsigned pg = (unsigned)(per_cu * cu_count());
+    const unsigned grid = items < pg ? items : pg;
+#define HJ_JOIN(W, WR, TSL, NT) hipLaunchKernelGGL((k_join<W, WR, TSL, NT>), dim3(grid), dim3(NT), 0, st, a)
+#define HJ_JOIN_V(W, WR)                              \
+    do {                                              \
+        if (jv.tsl == 13) HJ_JOIN(W, WR, 13, 1024);   \
+        else if (jv.tsl == 12) HJ_JOIN(W, WR, 12, 512); \
+        else HJ_JOIN(W, WR, 11, 256);                 \
+    } while (0)
     if (wide) {
-        if (count_only) hipLaunchKernelGGL((k_join<JWide, false>), dim3(grid), dim3(kJoinThreads), 0, st, a);
-        else hipLaunchKernelGGL((k_join<JWide, true>), dim3(grid), dim3(kJoinThreads), 0, st, a);
+        if (count_only) HJ_JOIN_V(true, false);
+        else HJ_JOIN_V(true, true);
     } else {
-        if (count_only) hipLaunchKernelGGL((k_join<JNarrow, false>), dim3(grid), dim3(kJoinThreads), 0, st, a);
-        else hipLaunchKernelGGL((k_join<JNarrow, true>), dim3(grid), dim3(kJoinThreads), 0, st, a);
+        if (count_only) HJ_JOIN_V(false, false);
+        else HJ_JOIN_V(false, true);
     }
+#undef HJ_JOIN_V
+#undef HJ_JOIN
     return hipGetLastError();
 }
 
