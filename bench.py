@@ -35,6 +35,7 @@ CONFIGS = {
     "C1": (26, 26, "pkfk", "PK-FK |R|=|S|=2^26 int64 key+payload, match fraction 1"),
     "C1-ref": (26, 26, "uniform", "uniform keys in [1,2^30] both sides, |R|=|S|=2^26 int64"),
     "C2": (20, 30, "pkfk", "PK-FK |R|=2^20 build, |S|=2^30 probe, int64"),
+    "C4": (28, 28, "zipf", "PK build |R|=2^28, Zipf(0.9) foreign keys |S|=2^28, int64"),
 }
 
 
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--verify", action="store_true", help="check the last step's output properties")
     ap.add_argument("--strategy", default="auto", choices=["auto", "global", "radix"])
     ap.add_argument("--radix-bits", type=int, default=0)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the multi-GPU code path (partition + all-to-all) even at N=1")
     return ap.parse_args()
 
 
@@ -94,8 +97,11 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    use_dist = world > 1 or a.force_dist
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
 
     import hashjoin
     from hashjoin.dist import distributed_join
@@ -106,23 +112,26 @@ def main():
     s0, ns = rank * NS // world, (rank + 1) * NS // world - rank * NS // world
     if distn == "pkfk":
         rk, rp, sk, sp = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, ns)
+    elif distn == "zipf":
+        rk, rp, _, _ = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, 0)
+        sk, sp = hashjoin.gen_zipf(a.seed, NR, NS, 0.9, s0, ns)
     else:
         rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)
         sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 1 << 30, ns, i0=s0)
     hj = hashjoin.HashJoin(local)
     hj.set_strategy(a.strategy, radix_bits=a.radix_bits)
-    expect_m = NS if distn == "pkfk" else None
+    expect_m = NS if distn in ("pkfk", "zipf") else None
     torch.cuda.synchronize()
 
     phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0,
               "partition+exchange": 0.0}
     last = {}
 
-    if world == 1:
+    if not use_dist:
         hj.allocate_hash_table(NR, 64)
         hj.build_table(rk, rp)
         hj.reserve_probe(NS, 64)
-        cap = NS if distn == "pkfk" else int(NR * NS / (1 << 30) * 1.1) + 4096
+        cap = NS if distn in ("pkfk", "zipf") else int(NR * NS / (1 << 30) * 1.1) + 4096
         out_r = torch.empty(cap, dtype=torch.int64, device="cuda")
         out_s = torch.empty_like(out_r)
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -154,18 +163,18 @@ def main():
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
     m_local = last["m"]
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([elapsed, float(m_local)], dtype=torch.float64, device="cuda")
         mx = tt.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = tt.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
@@ -175,7 +184,7 @@ def main():
     if expect_m is not None and m_total != expect_m:
         raise SystemExit(f"join produced {m_total} rows, expected {expect_m}")
 
-    if a.verify and world == 1:
+    if a.verify and not use_dist:
         o_r, o_s = out_r[:m_local], out_s[:m_local]
         assert bool((rk[o_r] == sk[o_s]).all()), "non-matching pair in output"
 
@@ -208,7 +217,8 @@ def main():
         "data": "synthetic (counter-based PK-FK generator, seed 0x5EED, generated on device)",
         "config": {"workload": f"{a.config}: {desc}", "R_rows": NR, "S_rows": NS, "key": "int64",
                    "payload": "int64", "distribution": distn,
-                   "parallelism": "single GPU" if world == 1 else f"radix-partitioned x{world}, RCCL all-to-all"},
+                   "parallelism": ("single GPU" if not use_dist
+                                   else f"radix-partitioned x{world}, RCCL all-to-all")},
         "joined_rows_per_sec": round(m_total / (ms / 1000.0), 1),
         "result_rows": m_total,
         "phase_ms": ph,
@@ -235,7 +245,7 @@ def main():
             "algorithmic_bytes_per_launch": (nr + ns) * 16 + m_local * 16,
             "achieved": round(((nr + ns) * 16 + m_local * 16) / (join_ms / 1000.0) / 1e9, 1), "unit": "GB/s"},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not use_dist and not a.no_cpu_baseline:
         threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
         line["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_sample_log2, threads)
     elif rank == 0:
@@ -243,7 +253,7 @@ def main():
     if rank == 0:
         print(json.dumps(line), flush=True)
     hj.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

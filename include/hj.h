@@ -142,6 +142,13 @@ int hj_partition_of(int64_t key, int nparts);
 int hj_dev_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_threshold,
                         int64_t r0, int64_t nr, int64_t *rkey, int64_t *rpay,
                         int64_t s0, int64_t ns, int64_t *skey, int64_t *spay, void *stream);
+/* Zipf(theta) probe keys over the PK-FK build side of the same seed: S.key =
+ * R.key[row(rank)], rank ~ Zipf(theta) over [0, NR) (Gray et al. inverse
+ * CDF), S.pay = global row.  hj_zipf_params returns
+ * {zeta(NR, theta), eta, alpha, 0.5^theta} (host, for the oracle). */
+int hj_zipf_params(int64_t NR, double theta, double out[4]);
+int hj_dev_gen_zipf_i64(uint64_t seed, int64_t NR, double theta, int64_t s0, int64_t ns, int64_t *skey,
+                        int64_t *spay, void *stream);
 int hj_dev_gen_uniform_i64(uint64_t seed, uint64_t stream_id, int64_t lo, int64_t hi,
                            int64_t i0, int64_t n, int64_t *key, int64_t *pay, void *stream);
 int hj_dev_gen_uniform_i32(uint64_t seed, uint64_t stream_id, int32_t lo, int32_t hi,

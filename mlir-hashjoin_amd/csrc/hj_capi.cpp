@@ -12,6 +12,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -749,6 +750,41 @@ int hj_dev_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_threshold, int64
                                (long long *)skey, (long long *)spay, (hipStream_t)stream));
     return HJ_OK;
 }
+int hj_zipf_params(int64_t NR, double theta, double out[4]) {
+    if (NR < 1 || !(theta > 0.0 && theta < 1.0) || !out) HJ_FAIL(HJ_ERR_ARG, "zipf: NR >= 1 and 0 < theta < 1");
+    // zeta(n, theta) = sum_{k=1..n} k^-theta: exact below 2^20 terms, then
+    // Euler-Maclaurin for the tail (relative error < 1e-12 at n = 2^28)
+    const int64_t m = NR < (1ll << 20) ? NR : (1ll << 20);
+    double z = 0.0;
+    for (int64_t k = m; k >= 1; --k) z += std::pow((double)k, -theta);
+    if (NR > m) {
+        const double a = (double)m, b = (double)NR, e = 1.0 - theta;
+        z += (std::pow(b, e) - std::pow(a, e)) / e + 0.5 * (std::pow(b, -theta) - std::pow(a, -theta)) -
+             theta / 12.0 * (std::pow(b, -theta - 1.0) - std::pow(a, -theta - 1.0));
+    }
+    double z2 = 1.0 + std::pow(2.0, -theta);
+    out[0] = z;
+    out[1] = (1.0 - std::pow(2.0 / (double)NR, 1.0 - theta)) / (1.0 - z2 / z);
+    out[2] = 1.0 / (1.0 - theta);
+    out[3] = std::pow(0.5, theta);
+    return HJ_OK;
+}
+
+int hj_dev_gen_zipf_i64(uint64_t seed, int64_t NR, double theta, int64_t s0, int64_t ns, int64_t *skey,
+                        int64_t *spay, void *stream) {
+    double p[4];
+    HJ_TRY(hj_zipf_params(NR, theta, p));
+    if (ns < 0) HJ_FAIL(HJ_ERR_ARG, "bad generator sizes");
+    hj::ZipfParams z;
+    z.zetan = p[0];
+    z.eta = p[1];
+    z.alpha = p[2];
+    z.half_pow_theta = p[3];
+    z.n = (unsigned long long)NR;
+    HJ_HIP(hj::launch_gen_zipf(seed, z, s0, ns, (long long *)skey, (long long *)spay, (hipStream_t)stream));
+    return HJ_OK;
+}
+
 int hj_dev_gen_uniform_i64(uint64_t seed, uint64_t stream_id, int64_t lo, int64_t hi, int64_t i0, int64_t n,
                            int64_t *key, int64_t *pay, void *stream) {
     if (hi < lo || n < 0) HJ_FAIL(HJ_ERR_ARG, "bad generator range");

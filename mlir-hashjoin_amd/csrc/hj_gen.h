@@ -4,6 +4,7 @@
 // reference itself seeds rand() from the clock (shared_stuff/shared.cpp:62,
 // :86-87), so there is no reproducible reference generator to follow.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -44,6 +45,35 @@ HJ_HD int64_t pkfk_skey(uint64_t seed, uint64_t salt, int64_t NR, uint64_t hit_t
     bool hit = (hit_thr == ~0ull) || (rand64(seed, 2, g) < hit_thr);
     uint64_t src = hit ? u : ((uint64_t)NR + g);
     return (int64_t)fmix64(src ^ salt);
+}
+
+// Zipf(theta) foreign keys over a unique build side: rank r
+// in [0, NR) is drawn by the inverse-CDF approximation of Gray et al.
+// ("Quickly generating billion-record synthetic databases", SIGMOD'94, the
+// YCSB generator); r -> build row via an odd-multiplier map so hot ranks land
+// on unrelated rows (and hash partitions).  S.key = R.key[row(r)].
+struct ZipfParams {
+    double zetan, eta, alpha, half_pow_theta;
+    unsigned long long n;
+};
+
+HJ_HD unsigned long long zipf_rank(const ZipfParams &z, double u) {
+    const double uz = u * z.zetan;
+    if (uz < 1.0) return 0ull;
+    if (uz < 1.0 + z.half_pow_theta) return 1ull;
+    double v = (double)z.n * pow(z.eta * u - z.eta + 1.0, z.alpha);
+    unsigned long long r = (unsigned long long)v;
+    return r >= z.n ? z.n - 1 : r;
+}
+
+HJ_HD uint64_t zipf_row(uint64_t seed, uint64_t rank, uint64_t NR) {
+    const uint64_t x = rank * 0x9E3779B97F4A7C15ull + mix64(seed ^ 0x2197ull);
+    return (NR & (NR - 1)) == 0 ? (x & (NR - 1)) : (x % NR);
+}
+
+HJ_HD int64_t zipf_skey(uint64_t seed, const ZipfParams &z, uint64_t g) {
+    const double u = (double)(rand64(seed, 3, g) >> 11) * (1.0 / 9007199254740992.0);   // [0, 1)
+    return pkfk_rkey(pkfk_salt(seed), zipf_row(seed, zipf_rank(z, u), z.n));
 }
 
 }  // namespace hj

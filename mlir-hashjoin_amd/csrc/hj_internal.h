@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hj_gen.h"
+
 namespace hj {
 
 constexpr unsigned long long kEmptyKey64 = 0x8000000000000000ull;
@@ -104,6 +106,8 @@ hipError_t launch_gen_pkfk(unsigned long long seed, long long NR, unsigned long 
                            long long r0, long long nr, long long *rkey, long long *rpay,
                            long long s0, long long ns, long long *skey, long long *spay,
                            hipStream_t st);
+hipError_t launch_gen_zipf(unsigned long long seed, const ZipfParams &z, long long s0, long long ns, long long *skey,
+                           long long *spay, hipStream_t st);
 hipError_t launch_gen_uniform_i64(unsigned long long seed, unsigned long long stream_id,
                                   long long lo, long long hi, long long i0, long long n,
                                   long long *key, long long *pay, hipStream_t st);

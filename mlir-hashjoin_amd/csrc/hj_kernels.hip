@@ -405,6 +405,15 @@ __global__ __launch_bounds__(kBlock) void k_gen_uniform_i32(unsigned long long s
     key[i] = (int)((long long)lo + (long long)(r % range));
 }
 
+__global__ __launch_bounds__(kBlock) void k_gen_zipf(unsigned long long seed, ZipfParams z, long long s0, long long ns,
+                                                     long long *skey, long long *spay) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= ns) return;
+    const unsigned long long g = (unsigned long long)(s0 + i);
+    skey[i] = zipf_skey(seed, z, g);
+    spay[i] = (long long)g;
+}
+
 inline unsigned grid_for(long long n, int per_block) {
     return (unsigned)((n + per_block - 1) / per_block);
 }
@@ -484,6 +493,13 @@ hipError_t launch_gen_pkfk(unsigned long long seed, long long NR, unsigned long 
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_gen_pkfk, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, seed, NR, hit_thr, r0, nr,
                        rkey, rpay, s0, ns, skey, spay);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_zipf(unsigned long long seed, const ZipfParams &z, long long s0, long long ns, long long *skey,
+                           long long *spay, hipStream_t st) {
+    if (ns <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_zipf, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, st, seed, z, s0, ns, skey, spay);
     return hipGetLastError();
 }
 

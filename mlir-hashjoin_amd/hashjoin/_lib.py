@@ -72,6 +72,8 @@ def _load():
         "hj_dev_partition_tuples_i64": (_int, [_vp, _vp, _i64, _int, _vp, _vp, _vp]),
         "hj_partition_of": (_int, [_i64, _int]),
         "hj_dev_gen_pkfk_i64": (_int, [_u64, _i64, _u64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+        "hj_zipf_params": (_int, [_i64, C.c_double, C.POINTER(C.c_double)]),
+        "hj_dev_gen_zipf_i64": (_int, [_u64, _i64, C.c_double, _i64, _i64, _vp, _vp, _vp]),
         "hj_dev_gen_uniform_i64": (_int, [_u64, _u64, _i64, _i64, _i64, _i64, _vp, _vp, _vp]),
         "hj_dev_gen_uniform_i32": (_int, [_u64, _u64, C.c_int32, C.c_int32, _i64, _i64, _vp, _vp]),
         "hj_count_i32": (_i64, [_vp, _vp, _i64, _i64, _i64] * 2),

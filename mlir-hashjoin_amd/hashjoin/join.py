@@ -226,6 +226,23 @@ def gen_pkfk(seed, NR, NS, frac=1.0, r0=0, nr=None, s0=0, ns=None, device=None, 
     return rk, rp, sk, sp
 
 
+def zipf_params(NR, theta):
+    a = (C.c_double * 4)()
+    check(lib.hj_zipf_params(int(NR), float(theta), a), "hj_zipf_params")
+    return list(a)
+
+
+def gen_zipf(seed, NR, NS, theta=0.9, s0=0, ns=None, device=None, stream=None):
+    """Slice [s0, s0+ns) of a Zipf(theta) probe side over the PK-FK build side
+    of the same seed (gen_pkfk's R), generated on the device."""
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    ns = NS if ns is None else ns
+    sk = torch.empty(ns, dtype=torch.int64, device=dev); sp = torch.empty_like(sk)
+    check(lib.hj_dev_gen_zipf_i64(seed, NR, float(theta), s0, ns, _ptr(sk), _ptr(sp), _stream(dev, stream)),
+          "hj_dev_gen_zipf_i64")
+    return sk, sp
+
+
 def gen_uniform_i64(seed, stream_id, lo, hi, n, i0=0, device=None, stream=None):
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
     k = torch.empty(n, dtype=torch.int64, device=dev); p = torch.empty_like(k)

@@ -19,6 +19,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -68,6 +69,33 @@ void oracle_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_thr,
         int hit = (hit_thr == UINT64_MAX) || (oracle_rand(seed, 2, g) < hit_thr);
         uint64_t src = hit ? u : ((uint64_t)NR + g);
         skey[j] = (int64_t)oracle_fmix64(src ^ salt);
+        spay[j] = (int64_t)g;
+    }
+}
+
+/* Zipf(theta) probe keys over the PK-FK build side of the same seed (the HIP
+ * generator's definition, mlir-hashjoin_amd/csrc/hj_gen.h; params from
+ * hj_zipf_params): rank by the Gray et al. inverse CDF, rank -> build row by an
+ * odd-multiplier map, S.key = R.key[row].  libm pow() may differ from the
+ * device's in the last ulp, so a rare rank can differ (tests allow it). */
+void oracle_gen_zipf_i64(uint64_t seed, int64_t NR, double zetan, double eta, double alpha, double half_pow_theta,
+                         int64_t s0, int64_t ns, int64_t *skey, int64_t *spay) {
+    const uint64_t salt = mix64(seed ^ 0x5EEDull);
+    for (int64_t j = 0; j < ns; ++j) {
+        const uint64_t g = (uint64_t)(s0 + j);
+        const double u = (double)(oracle_rand(seed, 3, g) >> 11) * (1.0 / 9007199254740992.0);
+        const double uz = u * zetan;
+        uint64_t r;
+        if (uz < 1.0) r = 0;
+        else if (uz < 1.0 + half_pow_theta) r = 1;
+        else {
+            const double v = (double)NR * pow(eta * u - eta + 1.0, alpha);
+            r = (uint64_t)v;
+            if (r >= (uint64_t)NR) r = (uint64_t)NR - 1;
+        }
+        const uint64_t x = r * 0x9E3779B97F4A7C15ull + mix64(seed ^ 0x2197ull);
+        const uint64_t row = ((NR & (NR - 1)) == 0) ? (x & (uint64_t)(NR - 1)) : (x % (uint64_t)NR);
+        skey[j] = (int64_t)oracle_fmix64(row ^ salt);
         spay[j] = (int64_t)g;
     }
 }

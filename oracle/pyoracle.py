@@ -45,6 +45,9 @@ def lib():
         L.oracle_rand.argtypes = [_u64, _u64, _u64]
         L.oracle_gen_pkfk_i64.restype = None
         L.oracle_gen_pkfk_i64.argtypes = [_u64, _i64, _u64, _i64, _i64, _i64p, _i64p, _i64, _i64, _i64p, _i64p]
+        L.oracle_gen_zipf_i64.restype = None
+        L.oracle_gen_zipf_i64.argtypes = [_u64, _i64, C.c_double, C.c_double, C.c_double, C.c_double, _i64, _i64,
+                                          _i64p, _i64p]
         L.oracle_gen_uniform_i64.restype = None
         L.oracle_gen_uniform_i64.argtypes = [_u64, _u64, _i64, _i64, _i64, _i64, _i64p, _i64p]
         L.oracle_gen_uniform_i32.restype = None
@@ -97,6 +100,13 @@ def gen_pkfk_i64(seed, NR, NS, frac=1.0, r0=0, nr=None, s0=0, ns=None):
     sk = np.empty(ns, np.int64); sp = np.empty(ns, np.int64)
     lib().oracle_gen_pkfk_i64(seed, NR, hit_threshold(frac), r0, nr, rk, rp, s0, ns, sk, sp)
     return rk, rp, sk, sp
+
+
+def gen_zipf_i64(seed, NR, params, s0=0, ns=0):
+    """params = hashjoin.zipf_params(NR, theta) (zeta, eta, alpha, 0.5^theta)."""
+    sk = np.empty(ns, np.int64); sp = np.empty(ns, np.int64)
+    lib().oracle_gen_zipf_i64(seed, NR, params[0], params[1], params[2], params[3], s0, ns, sk, sp)
+    return sk, sp
 
 
 def gen_uniform_i64(seed, stream, lo, hi, n, i0=0):
