@@ -62,6 +62,17 @@ int table_bits(int64_t n) {
     return b < 4 ? 4 : b;
 }
 
+// HJ_TRACE=1: synchronise and log every phase to stderr (diagnostics).
+bool trace_on() {
+    static const bool on = getenv("HJ_TRACE") != nullptr;
+    return on;
+}
+void trace(const char *what, hipStream_t st, long long n = -1) {
+    if (!trace_on()) return;
+    const hipError_t e = hipStreamSynchronize(st);
+    std::fprintf(stderr, "hj trace: %s n=%lld -> %s\n", what, n, hipGetErrorString(e));
+}
+
 enum Ev { kEvInit0, kEvInit1, kEvBuild1, kEvProbe0, kEvProbeMid, kEvProbe1, kEvPart0, kEvPart1, kEvCount };
 
 // Build sides at least this large use the radix-partitioned join (LDS
@@ -233,8 +244,10 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         record(c, kEvInit0, st);
         HJ_HIP(hipMemsetAsync(c->meta, 0, 2 * sizeof(unsigned long long), st));
         record(c, kEvInit1, st);
+        trace("build: workspace", st, src.n);
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->rrows.p, (unsigned long long *)c->r_off.p,
                                    st));
+        trace("build: R partitioned", st, (long long)c->plan.total_bits);
         record(c, kEvBuild1, st);
         c->rec[0] = c->rec[1] = c->timing;
         return HJ_OK;
@@ -265,17 +278,21 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         const size_t esz = wide ? 16 : 8;
         const size_t P = size_t(1) << c->plan.total_bits;
         const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
+        trace("probe: enter", st, src.n);
         HJ_TRY(ensure_buf(c->srows, rows * esz));
         HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
         HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
+        trace("probe: workspace", st, (long long)P);
         record(c, kEvProbe0, st);
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->srows.p, (unsigned long long *)c->s_off.p,
                                    st));
+        trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
         HJ_HIP(hj::radix_join(wide, c->plan, c->rrows.p, (const unsigned long long *)c->r_off.p, c->srows.p,
                               (const unsigned long long *)c->s_off.p, src.n, (unsigned *)c->work_start.p, out_r,
                               out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1, count_only,
                               st));
+        trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
         c->rec_mid = c->timing;

@@ -463,29 +463,26 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     Item it = item_of<CH>(a, w);
     T sv_[SI], rv_[RI];
 #pragma unroll
-    for (int i = 0; i < SI; ++i) {
-        const u64 row = it.s_lo + (u64)i * NT + threadIdx.x;
-        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
-    }
-#pragma unroll
     for (int i = 0; i < RI; ++i) {
         const u64 row = it.r_lo + (u64)i * NT + threadIdx.x;
         rv_[i] = row < it.r_hi ? rrows[row] : R::zero();
     }
 
     while (true) {
-        // ---- prefetch the next work item
+        // this item's first S sub-chunk: issued before the table init / build
+        // so its latency hides behind them
+#pragma unroll
+        for (int i = 0; i < SI; ++i) {
+            const u64 row = it.s_lo + (u64)i * NT + threadIdx.x;
+            sv_[i] = row < it.s_hi ? srows[row] : R::zero();
+        }
+        // ---- prefetch the next work item's build rows
         const unsigned wn = w + gridDim.x;
         const bool more = wn < total;
         Item nx;
-        T nsv[SI], nrv[RI];
+        T nrv[RI];
         if (more) {
             nx = item_of<CH>(a, wn);
-#pragma unroll
-            for (int i = 0; i < SI; ++i) {
-                const u64 row = nx.s_lo + (u64)i * NT + threadIdx.x;
-                nsv[i] = row < nx.s_hi ? srows[row] : R::zero();
-            }
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
                 const u64 row = nx.r_lo + (u64)i * NT + threadIdx.x;
@@ -690,8 +687,6 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
         if (!more) break;
         w = wn;
         it = nx;
-#pragma unroll
-        for (int i = 0; i < SI; ++i) sv_[i] = nsv[i];
 #pragma unroll
         for (int i = 0; i < RI; ++i) rv_[i] = nrv[i];
     }

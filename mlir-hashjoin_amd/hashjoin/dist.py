@@ -17,19 +17,70 @@ exchange logic is exercised with gloo on CPU tensors in tests/.
 """
 from __future__ import annotations
 
+import os
+import sys
+import time
+
 import torch
 import torch.distributed as dist
 
+_DEBUG = os.environ.get("HJ_DEBUG") == "1"
 
-def exchange(send_r, counts_r, send_s, counts_s, group=None):
+
+def _dbg(*a):
+    if _DEBUG:
+        torch.cuda.synchronize()
+        print(f"[hj.dist {time.time():.3f} rank {dist.get_rank()}]", *a, file=sys.stderr, flush=True)
+
+
+# Largest slice one rank hands one peer in one collective round.  RCCL moves
+# each point-to-point message with a 32-bit byte count internally on some
+# paths, so a 4 GiB slice (2^28 16-B tuples) is silently truncated; rounds of
+# at most 2^26 rows (1 GiB) stay well clear of that and are still large enough
+# to run xGMI at link rate.
+MAX_ROWS_PER_ROUND = 1 << 26
+
+
+def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows):
+    """recv[rows from p] <- every p's send[rows for me]: one batched group of
+    point-to-point messages of at most max_rows rows each (views, no staging
+    copies).  Sender and receiver cut a slice into the same pieces because
+    in_rows on p and out_rows here describe the same slice."""
+    world = len(in_rows)
+    me = dist.get_rank(group)
+    in_off = [sum(in_rows[:p]) for p in range(world)]
+    out_off = [sum(out_rows[:p]) for p in range(world)]
+    recv[out_off[me]:out_off[me] + out_rows[me]].copy_(send[in_off[me]:in_off[me] + in_rows[me]])
+    ops = []
+    for d in range(1, world):
+        # pair ranks by distance so every link carries traffic at once
+        to, fr = (me + d) % world, (me - d) % world
+        peer_to = dist.get_global_rank(group, to) if group is not None else to
+        peer_fr = dist.get_global_rank(group, fr) if group is not None else fr
+        for a in range(0, in_rows[to], max_rows):
+            b = min(in_rows[to], a + max_rows)
+            ops.append(dist.P2POp(dist.isend, send[in_off[to] + a:in_off[to] + b], peer_to, group))
+        for a in range(0, out_rows[fr], max_rows):
+            b = min(out_rows[fr], a + max_rows)
+            ops.append(dist.P2POp(dist.irecv, recv[out_off[fr] + a:out_off[fr] + b], peer_fr, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def exchange(send_r, counts_r, send_s, counts_s, group=None, max_rows=None):
     """All-to-all-v of two partitioned tuple buffers.
 
     send_x: (n, 2) int64 rows grouped by destination rank 0..P-1;
     counts_x: (P,) int64 rows per destination.  Returns (recv_r, recv_s, splits)
-    where recv_x holds the rows every rank routed here (grouped by source)."""
+    where recv_x holds the rows every rank routed here (grouped by source).
+    Slices larger than max_rows (default MAX_ROWS_PER_ROUND) move in rounds."""
     world = dist.get_world_size(group)
     if counts_r.numel() != world or counts_s.numel() != world:
         raise ValueError("one count per rank required")
+    max_rows = MAX_ROWS_PER_ROUND if max_rows is None else int(max_rows)
+    if max_rows < 1:
+        raise ValueError("max_rows must be positive")
     both = torch.stack([counts_r, counts_s], dim=1).reshape(-1).contiguous()
     recv_both = torch.empty_like(both)
     dist.all_to_all_single(recv_both, both, group=group)
@@ -38,8 +89,8 @@ def exchange(send_r, counts_r, send_s, counts_s, group=None):
     out_r, out_s = host[1, :, 0].tolist(), host[1, :, 1].tolist()
     recv_r = torch.empty((sum(out_r), 2), dtype=torch.int64, device=send_r.device)
     recv_s = torch.empty((sum(out_s), 2), dtype=torch.int64, device=send_s.device)
-    dist.all_to_all_single(recv_r, send_r, out_r, in_r, group=group)
-    dist.all_to_all_single(recv_s, send_s, out_s, in_s, group=group)
+    _all_to_all_rows(recv_r, send_r, out_r, in_r, group, max_rows)
+    _all_to_all_rows(recv_s, send_s, out_s, in_s, group, max_rows)
     return recv_r, recv_s, {"in_r": in_r, "in_s": in_s, "out_r": out_r, "out_s": out_s}
 
 
@@ -53,13 +104,17 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     world = dist.get_world_size(group)
     ev = (lambda name: _event(phases, name)) if phases is not None else (lambda name: None)
     ev("start")
+    _dbg("partition", rkey.numel(), skey.numel())
     send_r, cr = hj.partition(rkey, rpay, world)
     send_s, cs = hj.partition(skey, spay, world)
     ev("partitioned")
+    _dbg("exchange", cr.tolist() if _DEBUG else None, cs.tolist() if _DEBUG else None)
     recv_r, recv_s, _ = exchange(send_r, cr, send_s, cs, group)
     ev("exchanged")
+    _dbg("build", recv_r.shape[0], recv_s.shape[0])
     hj.build_tuples(recv_r)
     ev("built")
+    _dbg("probe")
     cap = max(1, recv_s.shape[0] if capacity is None else int(capacity))
     for _ in range(2):
         out_r = torch.empty(cap, dtype=torch.int64, device=recv_s.device)

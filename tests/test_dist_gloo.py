@@ -56,7 +56,7 @@ def _worker(rank, world, port, case, outdir):
         sk, sp = O.gen_uniform_i64(case["seed"], 2, 1, case["hi"], ns, i0=s0)
     send_r, cr = _route(rk, rp, world)
     send_s, cs = _route(sk, sp, world)
-    recv_r, recv_s, splits = exchange(send_r, cr, send_s, cs)
+    recv_r, recv_s, splits = exchange(send_r, cr, send_s, cs, max_rows=case.get("max_rows"))
     assert sum(splits["out_r"]) == recv_r.shape[0]
     # every received row is owned by this rank
     from test_abi import _np_partition_of
@@ -76,9 +76,11 @@ def _worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=11),
     dict(dist="uniform", NR=2000, NS=2500, hi=300, seed=12),      # duplicates both sides
     dict(dist="pkfk", NR=7, NS=3, frac=1.0, seed=13),             # tiny / ragged
-], ids=["pkfk", "uniform_dups", "tiny"])
+    dict(dist="pkfk", NR=3001, NS=4999, frac=0.7, seed=14, max_rows=97),  # slices cut in pieces
+    dict(dist="pkfk", NR=4000, NS=6001, frac=0.9, seed=15, max_rows=300, world=3),
+], ids=["pkfk", "uniform_dups", "tiny", "pieces", "three_ranks_pieces"])
 def test_two_rank_exchange_join(case, tmp_path, oracle):
-    world = 2
+    world = case.get("world", 2)
     mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
     rs, ss, tot_r, tot_s = [], [], 0, 0
     for k in range(world):
