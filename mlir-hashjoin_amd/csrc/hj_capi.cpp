@@ -84,6 +84,13 @@ struct Buf {
     size_t bytes = 0;
 };
 
+// Device buffers of one radix bucket set (hj::BucketSet).
+struct SetBufs {
+    Buf rows, bbin, bfill, blist, pstart;
+    unsigned max_buckets = 0;
+    unsigned long long max_rows = 0;
+};
+
 }  // namespace
 
 struct hj_ctx {
@@ -103,7 +110,8 @@ struct hj_ctx {
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
-    Buf rrows, srows, tmp, off_a, off_b, r_off, s_off, tile_start, tile_owner, work_start, hist, scan_sums;
+    SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
+    Buf nb, pcur, tile_start, tile_owner, work_start, scan_sums;
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -186,31 +194,57 @@ void free_buf(Buf &b) {
     b.bytes = 0;
 }
 
-// Partition scratch sized for n rows under plan pl (shared by R and S).
-int ensure_radix_scratch(hj_ctx *c, int64_t n, size_t esz, const hj::RadixPlan &pl) {
+int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
+    if (need.buckets > 0xFFFFFFF0ull) HJ_FAIL(HJ_ERR_CAPACITY, "radix partition: too many buckets");
+    HJ_TRY(ensure_buf(sb.rows, (size_t)need.rows * esz));
+    HJ_TRY(ensure_buf(sb.bbin, (size_t)need.buckets * 4));
+    HJ_TRY(ensure_buf(sb.bfill, (size_t)need.buckets * 4));
+    HJ_TRY(ensure_buf(sb.blist, (size_t)need.buckets * 8));
+    HJ_TRY(ensure_buf(sb.pstart, (P + 1) * 8));
+    // capacity actually held (buffers may be larger than this need)
+    size_t cap = sb.bbin.bytes / 4;
+    if (sb.bfill.bytes / 4 < cap) cap = sb.bfill.bytes / 4;
+    if (sb.blist.bytes / 8 < cap) cap = sb.blist.bytes / 8;
+    sb.max_buckets = (unsigned)(cap < 0xFFFFFFF0ull ? cap : 0xFFFFFFF0ull);
+    sb.max_rows = sb.rows.bytes / esz;
+    return HJ_OK;
+}
+
+hj::BucketSet bucket_set(SetBufs &sb) {
+    hj::BucketSet b;
+    b.rows = sb.rows.p;
+    b.bbin = (unsigned *)sb.bbin.p;
+    b.bfill = (unsigned *)sb.bfill.p;
+    b.blist = (unsigned long long *)sb.blist.p;
+    b.pstart = (unsigned long long *)sb.pstart.p;
+    b.max_buckets = sb.max_buckets;
+    b.max_rows = sb.max_rows;
+    return b;
+}
+
+// Partition scratch for n rows under plan pl (shared by R and S), plus the
+// relation's own final set.
+int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const hj::RadixPlan &pl) {
     const size_t P = size_t(1) << pl.total_bits;
-    const size_t rows = (size_t)(n > 0 ? n : 1);
-    if (pl.passes > 1) HJ_TRY(ensure_buf(c->tmp, rows * esz));
-    HJ_TRY(ensure_buf(c->off_a, (P + 1) * 8));
-    HJ_TRY(ensure_buf(c->off_b, (P + 1) * 8));
+    HJ_TRY(ensure_set(fin, hj::radix_need(n, pl, true), esz, P));
+    if (pl.passes > 1) HJ_TRY(ensure_set(c->tset, hj::radix_need(n, pl, false), esz, P));
+    HJ_TRY(ensure_buf(c->nb, 16));
+    HJ_TRY(ensure_buf(c->pcur, (P + 1) * 8));
     HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
-    HJ_TRY(ensure_buf(c->tile_owner, ((size_t)(n > 0 ? n : 1) / 4096 + P + 2) * 4));
+    HJ_TRY(ensure_buf(c->tile_owner, (size_t)hj::radix_tiles(n, (int)P) * 4));
     // work map: P + 1 chunk starts, then the item -> partition owner list
-    HJ_TRY(ensure_buf(c->work_start, (P + 1 + (size_t)(n > 0 ? n : 1) / (size_t)hj::radix_chunk_rows() + P + 2) * 4));
-    const size_t he = hj::radix_hist_elems(n, (int)P);
-    HJ_TRY(ensure_buf(c->hist, he * 8));
-    HJ_TRY(ensure_buf(c->scan_sums, (he / 8192 + 2) * 8));
+    HJ_TRY(ensure_buf(c->work_start, (P + 1 + (size_t)hj::radix_join_items(pl, fin.max_buckets)) * 4));
+    HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
     return HJ_OK;
 }
 
 hj::RadixWork radix_work(hj_ctx *c) {
     hj::RadixWork w;
-    w.tmp = c->tmp.p;
-    w.off_a = (unsigned long long *)c->off_a.p;
-    w.off_b = (unsigned long long *)c->off_b.p;
+    w.tmp = bucket_set(c->tset);
+    w.nb = (unsigned *)c->nb.p;
+    w.pcur = (unsigned long long *)c->pcur.p;
     w.tile_start = (unsigned *)c->tile_start.p;
     w.tile_owner = (unsigned *)c->tile_owner.p;
-    w.hist = (unsigned long long *)c->hist.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
     return w;
 }
@@ -236,17 +270,12 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;   // packed partitioned rows
         c->plan = hj::radix_plan(src.n, c->radix_bits);
-        const size_t P = size_t(1) << c->plan.total_bits;
-        const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
-        HJ_TRY(ensure_buf(c->rrows, rows * esz));
-        HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
-        HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
+        HJ_TRY(ensure_radix_scratch(c, c->rset, src.n, esz, c->plan));
         record(c, kEvInit0, st);
         HJ_HIP(hipMemsetAsync(c->meta, 0, 2 * sizeof(unsigned long long), st));
         record(c, kEvInit1, st);
         trace("build: workspace", st, src.n);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->rrows.p, (unsigned long long *)c->r_off.p,
-                                   st));
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->rset), st));
         trace("build: R partitioned", st, (long long)c->plan.total_bits);
         record(c, kEvBuild1, st);
         c->rec[0] = c->rec[1] = c->timing;
@@ -276,22 +305,16 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     if (c->used == HJ_STRATEGY_RADIX) {
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;
-        const size_t P = size_t(1) << c->plan.total_bits;
-        const size_t rows = (size_t)(src.n > 0 ? src.n : 1);
         trace("probe: enter", st, src.n);
-        HJ_TRY(ensure_buf(c->srows, rows * esz));
-        HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
-        HJ_TRY(ensure_radix_scratch(c, src.n, esz, c->plan));
-        trace("probe: workspace", st, (long long)P);
+        HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, esz, c->plan));
+        trace("probe: workspace", st, (long long)c->sset.max_buckets);
         record(c, kEvProbe0, st);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), c->srows.p, (unsigned long long *)c->s_off.p,
-                                   st));
+        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
-        HJ_HIP(hj::radix_join(wide, c->plan, c->rrows.p, (const unsigned long long *)c->r_off.p, c->srows.p,
-                              (const unsigned long long *)c->s_off.p, src.n, (unsigned *)c->work_start.p, out_r,
-                              out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1, count_only,
-                              st));
+        HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_buckets,
+                              (unsigned *)c->work_start.p, out_r, out_s, count_only ? 0 : cap,
+                              (unsigned long long *)d_count, c->meta + 1, count_only, st));
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
@@ -583,9 +606,9 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (int i = 0; i < 6; ++i)
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
-    for (Buf *b : {&c->rrows, &c->srows, &c->tmp, &c->off_a, &c->off_b, &c->r_off, &c->s_off,
-                   &c->tile_start, &c->tile_owner, &c->work_start, &c->hist, &c->scan_sums})
-        free_buf(*b);
+    for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
+        for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
+    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->scan_sums}) free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
     {
@@ -608,11 +631,7 @@ int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
         return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
     const size_t esz = key_bits == 64 ? 16 : 8;
     const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits);
-    const size_t P = size_t(1) << pl.total_bits;
-    const size_t rows = (size_t)(max_build_rows > 0 ? max_build_rows : 1);
-    HJ_TRY(ensure_buf(c->rrows, rows * esz));
-    HJ_TRY(ensure_buf(c->r_off, (P + 1) * 8));
-    return ensure_radix_scratch(c, max_build_rows, esz, pl);
+    return ensure_radix_scratch(c, c->rset, max_build_rows, esz, pl);
 }
 
 int64_t hj_ctx_table_capacity(const hj_ctx *c) {
@@ -697,11 +716,7 @@ int hj_ctx_reserve_probe(hj_ctx *c, int64_t max_probe_rows, int key_bits) {
     if (c->layout < 0 || c->used != HJ_STRATEGY_RADIX) return HJ_OK;   // the global table needs no probe workspace
     HJ_TRY(set_device(c));
     const size_t esz = key_bits == 64 ? 16 : 8;
-    const size_t P = size_t(1) << c->plan.total_bits;
-    const size_t rows = (size_t)(max_probe_rows > 0 ? max_probe_rows : 1);
-    HJ_TRY(ensure_buf(c->srows, rows * esz));
-    HJ_TRY(ensure_buf(c->s_off, (P + 1) * 8));
-    return ensure_radix_scratch(c, max_probe_rows, esz, c->plan);
+    return ensure_radix_scratch(c, c->sset, max_probe_rows, esz, c->plan);
 }
 
 // ------------------------------------------------------------ device phases

@@ -71,32 +71,52 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
 // ---------------------------------------------------------------- radix join
 // (hj_radix.hip) partitions both relations by the top bits of the key hash
 // until a partition's build rows fit one workgroup's LDS table, then joins
-// partition pairs in LDS.
+// partition pairs in LDS.  A pass writes rows into fixed-size buckets (one
+// partition per bucket, bucket chaining): no histogram pass, no global scan.
 struct RadixPlan {
     int passes;       // 1..3 partition passes
-    int bits[3];      // fan-out bits per pass (<= 8 each)
+    int bits[3];      // fan-out bits per pass (<= 9 each)
+    int pbl[3];       // log2 rows per bucket written by each pass
     int total_bits;   // P = 2^total_bits partitions
 };
 
+// One pass's output: packed rows in buckets of 2^pbl rows; bucket j holds
+// bfill[j] rows of partition bbin[j].  After the pass, blist lists the
+// buckets grouped by partition as (j << 32 | bfill[j]): partition p owns
+// blist[pstart[p] .. pstart[p+1]).
+struct BucketSet {
+    void *rows;                    // >= max_buckets << pbl rows
+    unsigned *bbin, *bfill;        // >= max_buckets
+    unsigned long long *blist;     // >= max_buckets
+    unsigned long long *pstart;    // >= P + 1 (P of the pass writing the set)
+    unsigned max_buckets;          // bbin / bfill / blist entries
+    unsigned long long max_rows;   // rows entries
+};
+
 struct RadixWork {                 // scratch shared by the partition passes
-    void *tmp;                     // ping buffer of packed rows (multi-pass plans), >= n rows
-    unsigned long long *off_a, *off_b;   // segment offsets, >= 2^total_bits + 1
-    unsigned *tile_start;          // >= 2^total_bits + 1
-    unsigned *tile_owner;          // >= n / 4096 + 2^total_bits + 1
-    unsigned long long *hist;      // >= radix_hist_elems(n, 2^total_bits)
-    unsigned long long *scan_sums; // >= hist elems / 8192 + 1
+    BucketSet tmp;                 // ping set of multi-pass plans
+    unsigned *nb;                  // device bucket counter
+    unsigned long long *pcur;      // >= P + 1: list placement cursors / chunk-map scratch
+    unsigned *tile_start;          // >= P + 1
+    unsigned *tile_owner;          // >= radix_tiles(n, P)
+    unsigned long long *scan_sums; // >= P / 8192 + 2
+};
+
+struct RadixNeed {                 // sizes of one bucket set
+    unsigned long long buckets, rows;
 };
 
 RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0: fixed 2^bits partitions
-size_t radix_hist_elems(long long n, int max_nseg);
-int radix_chunk_rows();
+// Bucket capacity of the final set (`final_set`) or the ping set of plan pl for n rows.
+RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set);
+unsigned long long radix_tiles(long long n, int max_nseg);
+unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets);
 // Partitioned rows are packed: 16 B {key, pay} (wide) or 8 B key << 32 | row id (narrow).
-hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out,
-                           unsigned long long *out_off, hipStream_t st);
-hipError_t radix_join(bool wide, const RadixPlan &pl, const void *r_rows, const unsigned long long *r_off,
-                      const void *s_rows, const unsigned long long *s_off, long long n_s, unsigned *work_start,
-                      void *out_r, void *out_s, long long cap, unsigned long long *counter,
-                      unsigned long long *dup_flag, bool count_only, hipStream_t st);
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
+                           const BucketSet &out, hipStream_t st);
+hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
+                      unsigned s_buckets, unsigned *work_start, void *out_r, void *out_s, long long cap,
+                      unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st);
 
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,

@@ -8,21 +8,25 @@
 // until a partition's build side fits one workgroup's LDS turns every HBM
 // access into a streaming, coalesced one; the hash table lives only in LDS.
 //
-//   pass k (1..3): tile histogram  ->  exclusive scan  ->  scatter (counting
-//                  sort of a 4096-row tile in LDS, then runs of rows written
-//                  contiguously to their partition)  ->  next segment offsets
-//   join:          one work item per (partition, S chunk): build the
-//                  partition's R rows into an LDS table, probe the chunk's S
-//                  rows, count, block-scan, reserve the block's output with
-//                  ONE global atomic, and write every pair at its position.
+//   pass k (1..3): bucket chaining.  A workgroup owns a contiguous range of
+//                  8192-row tiles; it counting-sorts each tile by bin in LDS
+//                  and appends every bin's run to the workgroup's current
+//                  bucket for that bin (2^pbl rows; a full bucket is replaced
+//                  by fresh ones from one global atomic counter).  The input
+//                  is read ONCE: no histogram pass and no global scan
+//                  (profiles/r01_micro_bucket_pass.txt: 2.27 ms per 2^28-row
+//                  pass vs 3.3 ms for histogram + exact-offset scatter).
+//                  Then the buckets are listed per partition (two small
+//                  kernels over ~n/512 bucket ids).
+//   join:          one work item per (partition, S bucket chunk): build the
+//                  partition's R buckets into an LDS table (rounds of RCAP
+//                  rows for oversized partitions), probe the chunk, count,
+//                  block-scan, reserve the block's output with ONE global
+//                  atomic, and write every pair at its position.
 //
 // Partitioned rows are packed: 16-B {key, payload} (64-bit keys) or 8-B
 // (key << 32 | row id) (the reference's i32 types), so a row moves with one
 // global load/store and an i32 row is already its own LDS table entry.
-//
-// Scatter and join are persistent (2 workgroups per CU) and software-
-// pipelined: the next tile / work item is loaded into registers before the
-// current one's LDS phase, so HBM latency hides behind LDS work.
 //
 // The reference's count -> prefix -> probe protocol (join_v1.mlir:288-521) is
 // kept, but per workgroup and on LDS, so the output needs no staging buffer
@@ -38,12 +42,17 @@ namespace {
 
 typedef unsigned long long u64;
 constexpr u64 kGold = 0x9E3779B97F4A7C15ull;
-constexpr int kTile = 4096;        // rows per partition-pass tile
-constexpr int kPassThreads = 512;  // 8 rows per thread
+constexpr int kTile = 8192;        // rows per partition-pass tile (LDS staging: 128 KiB wide)
+constexpr int kPassThreads = 1024; // one workgroup per CU
 constexpr int kPassRows = kTile / kPassThreads;
-constexpr int kJoinItems = 4;      // S rows per thread per sub-chunk of the join kernel
+constexpr int kMaxFan = 512;       // bins per pass (9 bits)
+constexpr int kJoinItems = 5;      // S rows per thread per sub-chunk of the join kernel (2560 rows = 10 buckets)
 constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build serves all)
-constexpr int kPackedRow = 3;      // SrcForm of partition-pass outputs (packed rows)
+constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
+constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
+constexpr unsigned kNoBucket = 0xFFFFFFFFu;
+constexpr int kPassPbl = 9;        // 512-row buckets for intermediate passes
+constexpr int kFinalPbl = 8;       // 256-row buckets for the join's input (less slack)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
 
@@ -113,45 +122,29 @@ __device__ __forceinline__ u64 block_excl_scan(u64 v, u64 *wsum, u64 *total) {
 }
 
 // --------------------------------------------------------------- maps
-// start[s] = sum over s' < s of count(s'), count(s) = ceil(len_a(s) / chunk),
-// or 0 when off_b is given and segment s of b is empty (no build rows ->
-// nothing to join).  One block of 1024 threads.
-__global__ __launch_bounds__(1024) void k_chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk,
-                                                    unsigned *start) {
-    __shared__ u64 wsum[16];
-    const int per = (nseg + 1023) / 1024;
-    const int s0 = threadIdx.x * per;
-    u64 local = 0;
-    for (int s = s0; s < s0 + per && s < nseg; ++s) {
-        const u64 len = off_a[s + 1] - off_a[s];
-        const bool live = off_b ? (off_b[s + 1] > off_b[s]) : true;
-        local += live ? (len + chunk - 1) / chunk : 0ull;
-    }
-    u64 total;
-    u64 run = block_excl_scan<1024>(local, wsum, &total);
-    for (int s = s0; s < s0 + per && s < nseg; ++s) {
-        start[s] = (unsigned)run;
-        const u64 len = off_a[s + 1] - off_a[s];
-        const bool live = off_b ? (off_b[s + 1] > off_b[s]) : true;
-        run += live ? (len + chunk - 1) / chunk : 0ull;
-    }
-    if (threadIdx.x == 0) start[nseg] = (unsigned)total;
-}
-
-// item -> segment list from a chunk map (start[] as written by k_chunk_map):
-// one thread per segment writes its items' owner, so consumers need a single
-// load instead of a log2(nseg)-step dependent binary search.
-__global__ __launch_bounds__(256) void k_work_list(const unsigned *start, int nseg, unsigned *owner) {
+// Chunk map of nseg segments: count(s) = ceil(len_a(s) / chunk), or 0 when
+// off_b is given and segment s of b is empty (no build rows -> nothing to
+// join); start = exclusive scan of count (scan_u64), and owner[w] = the
+// segment of chunk w, so consumers need one load instead of a search.
+__global__ __launch_bounds__(256) void k_chunk_count(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk,
+                                                     u64 *cnt) {
     const int s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= nseg) return;
-    for (unsigned w = start[s]; w < start[s + 1]; ++w) owner[w] = (unsigned)s;
+    if (s > nseg) return;
+    if (s == nseg) {
+        cnt[s] = 0;
+        return;
+    }
+    const u64 len = off_a[s + 1] - off_a[s];
+    const bool live = off_b ? (off_b[s + 1] > off_b[s]) : true;
+    cnt[s] = live ? (len + chunk - 1) / chunk : 0ull;
 }
 
-__global__ void k_set_off(u64 *off, u64 n) {
-    if (threadIdx.x == 0) {
-        off[0] = 0;
-        off[1] = n;
-    }
+__global__ __launch_bounds__(256) void k_chunk_finish(const u64 *scan, int nseg, unsigned *start, unsigned *owner) {
+    const int s = blockIdx.x * 256 + threadIdx.x;
+    if (s > nseg) return;
+    start[s] = (unsigned)scan[s];
+    if (s < nseg)
+        for (u64 w = scan[s]; w < scan[s + 1]; ++w) owner[w] = (unsigned)s;
 }
 
 // --------------------------------------------------------------- scan
@@ -201,132 +194,134 @@ __global__ __launch_bounds__(1024) void k_scan_add(u64 *a, u64 n, const u64 *sum
 
 // --------------------------------------------------------------- partition pass
 struct PassArgs {
-    SrcDev in;                   // pass input (key/pay/row_base/form; n unused)
-    const u64 *seg_off;          // nseg + 1
-    int nseg;
+    SrcDev in;                   // pass-1 source (FORM != kBucketed)
+    u64 n;                       // pass-1 source rows
+    // FORM == kBucketed: the previous pass's set, tiles of up to kTile rows
+    // (kTile >> in_pbl buckets) that never straddle two segments
+    const void *in_rows;
+    const u64 *in_list;          // bucket << 32 | fill
+    const u64 *in_pstart;
+    int in_pbl;
     const unsigned *tile_start;  // nseg + 1
-    const unsigned *tile_owner;  // tile -> segment (nseg > 1)
-    u64 *hist;                   // [seg][bin][tile] counts, then exclusive offsets
-    void *out;                   // packed rows
-    u64 *next_off;               // nseg * F + 1
+    const unsigned *tile_owner;  // tile -> segment
+    int nseg;
+    // output set
+    void *out_rows;
+    unsigned *bbin, *bfill, *nb;
+    unsigned max_buckets;
+    int out_pbl;
     int shift;                   // bin = (hash >> shift) & (F - 1)
     int fbits;
 };
 
-struct TileRange {
+struct PassTile {
     int seg;
-    unsigned t, ntiles;
-    u64 lo, hi;
+    u64 lo, hi;                  // source rows, or bucket-list positions (kBucketed)
 };
 
-__device__ __forceinline__ TileRange tile_range(const PassArgs &a, unsigned wg) {
-    TileRange r;
-    r.seg = a.nseg == 1 ? 0 : (int)a.tile_owner[wg];
-    r.t = wg - a.tile_start[r.seg];
-    r.ntiles = a.tile_start[r.seg + 1] - a.tile_start[r.seg];
-    r.lo = a.seg_off[r.seg] + (u64)r.t * kTile;
-    const u64 e = a.seg_off[r.seg + 1];
-    r.hi = r.lo + kTile < e ? r.lo + kTile : e;
+template <int FORM>
+__device__ __forceinline__ unsigned pass_tiles(const PassArgs &a) {
+    if constexpr (FORM == kBucketed) return a.tile_start[a.nseg];
+    else return (unsigned)((a.n + kTile - 1) / kTile);
+}
+
+template <int FORM>
+__device__ __forceinline__ PassTile pass_tile(const PassArgs &a, unsigned t) {
+    PassTile r;
+    if constexpr (FORM == kBucketed) {
+        r.seg = a.nseg == 1 ? 0 : (int)a.tile_owner[t];
+        const unsigned bpt = (unsigned)kTile >> a.in_pbl;
+        r.lo = a.in_pstart[r.seg] + (u64)(t - a.tile_start[r.seg]) * bpt;
+        const u64 e = a.in_pstart[r.seg + 1];
+        r.hi = r.lo + bpt < e ? r.lo + bpt : e;
+    } else {
+        r.seg = 0;
+        r.lo = (u64)t * kTile;
+        r.hi = r.lo + kTile < a.n ? r.lo + kTile : a.n;
+    }
     return r;
 }
 
-// Per-tile bin counts.  Keys are read 16 B per lane (two keys of a key
-// column, or the key half of one packed row).
+// Row v (0 <= v < kTile) of a tile; false if the tile has no such row.
 template <bool WIDE, int FORM>
-__global__ __launch_bounds__(kPassThreads) void k_hist(PassArgs a) {
+__device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, unsigned v, typename Row<WIDE>::T &out) {
     typedef Row<WIDE> R;
-    __shared__ unsigned cnt[512];
-    const unsigned wg = blockIdx.x;
-    if (wg >= a.tile_start[a.nseg]) return;   // upper-bound grid
-    const TileRange tr = tile_range(a, wg);
-    const unsigned F = 1u << a.fbits;
-    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) cnt[b] = 0u;
-    __syncthreads();
-    auto bin_of = [&](u64 k) { return (unsigned)(rhash(k) >> a.shift) & (F - 1); };
-    if constexpr (FORM == kCols64) {
-        // two consecutive keys per lane (one 16-B load): rows lo + 2*(i*NT + tid) + {0,1}
-        const bool al = ((((uintptr_t)a.in.key) & 15) == 0) && ((tr.lo & 1) == 0);
-#pragma unroll
-        for (int i = 0; i < kPassRows / 2; ++i) {
-            const u64 row = tr.lo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
-            if (al && row + 1 < tr.hi) {
-                const ulonglong2 kk = *(const ulonglong2 *)((const u64 *)a.in.key + row);
-                atomicAdd(&cnt[bin_of(kk.x)], 1u);
-                atomicAdd(&cnt[bin_of(kk.y)], 1u);
-            } else {
-                if (row < tr.hi) atomicAdd(&cnt[bin_of(((const u64 *)a.in.key)[row])], 1u);
-                if (row + 1 < tr.hi) atomicAdd(&cnt[bin_of(((const u64 *)a.in.key)[row + 1])], 1u);
-            }
-        }
+    if constexpr (FORM == kBucketed) {
+        const u64 li = t.lo + (v >> a.in_pbl);
+        if (li >= t.hi) return false;
+        const u64 e = a.in_list[li];
+        const unsigned off = v & ((1u << a.in_pbl) - 1u);
+        if (off >= (unsigned)e) return false;
+        out = ((const typename R::T *)a.in_rows)[((e >> 32) << a.in_pbl) + off];
+        return true;
     } else {
-#pragma unroll
-        for (int i = 0; i < kPassRows; ++i) {
-            const u64 row = tr.lo + (u64)i * kPassThreads + threadIdx.x;
-            if (row < tr.hi) atomicAdd(&cnt[bin_of(R::key(load_row<WIDE, FORM>(a.in, (long long)row)))], 1u);
-        }
+        const u64 row = t.lo + v;
+        if (row >= t.hi) return false;
+        out = load_row<WIDE, FORM>(a.in, (long long)row);
+        return true;
     }
-    __syncthreads();
-    const u64 base = (u64)a.tile_start[tr.seg] * F;
-    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) a.hist[base + (u64)b * tr.ntiles + tr.t] = cnt[b];
 }
 
-// Counting sort of each tile by bin in LDS, then contiguous runs written to
-// the bins' scanned output offsets.  Persistent: a workgroup walks tiles
-// wg, wg + grid, ... and loads the next tile's rows before sorting this one.
+// One partition pass (see the file header).  Workgroup w owns tiles
+// [w*T/G, (w+1)*T/G); its open bucket per bin lives in LDS (cur, fill) and
+// is closed (bfill written) when the workgroup moves to another segment or
+// finishes, so at most (G + nseg) * F buckets are ever partly filled.
 template <bool WIDE, int FORM>
-__global__ __launch_bounds__(kPassThreads, 4) void k_scatter(PassArgs a) {   // 2 workgroups per CU: <= 128 VGPRs
+__global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     constexpr int IT = kPassRows;
     __shared__ T stage[kTile];
     __shared__ unsigned short sb[kTile];
-    __shared__ unsigned cnt[512];
-    __shared__ long long dst_base[512];
-    const unsigned total = a.tile_start[a.nseg];
-    unsigned wg = blockIdx.x;
-    if (wg >= total) return;
+    __shared__ unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan], nbase[kMaxFan];
     const unsigned F = 1u << a.fbits;
-    T *out = (T *)a.out;
-
-    TileRange tr = tile_range(a, wg);
-    T row[IT];
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-        const u64 r = tr.lo + (u64)i * kPassThreads + threadIdx.x;
-        row[i] = r < tr.hi ? load_row<WIDE, FORM>(a.in, (long long)r) : R::zero();
+    const unsigned PB = 1u << a.out_pbl;
+    const unsigned T_ = pass_tiles<FORM>(a);
+    const unsigned t0 = (unsigned)((u64)blockIdx.x * T_ / gridDim.x);
+    const unsigned t1 = (unsigned)((u64)(blockIdx.x + 1) * T_ / gridDim.x);
+    T *out = (T *)a.out_rows;
+    for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
+        cnt[b] = 0u;
+        cur[b] = kNoBucket;
+        fill[b] = PB;
     }
-    while (true) {
-        // prefetch the next tile
-        const unsigned wn = wg + gridDim.x;
-        const bool more = wn < total;
-        TileRange tn;
-        T nrow[IT];
-        if (more) {
-            tn = tile_range(a, wn);
-#pragma unroll
-            for (int i = 0; i < IT; ++i) {
-                const u64 r = tn.lo + (u64)i * kPassThreads + threadIdx.x;
-                nrow[i] = r < tn.hi ? load_row<WIDE, FORM>(a.in, (long long)r) : R::zero();
-            }
+    int seg_cur = -1;
+    // close this workgroup's open buckets (their fill is final)
+    auto close_all = [&]() {
+        for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
+            if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = fill[b];
+            cur[b] = kNoBucket;
+            fill[b] = PB;
         }
-        // ---- sort this tile
-        for (unsigned b = threadIdx.x; b < F; b += kPassThreads) cnt[b] = 0u;
-        __syncthreads();
-        unsigned br[IT];   // bin << 16 | rank within the tile's bin (bin < 512, rank < 4096)
+    };
+    for (unsigned t = t0; t < t1; ++t) {
+        const PassTile tl = pass_tile<FORM>(a, t);
+        if (tl.seg != seg_cur) {   // uniform: every thread sees the same tile
+            __syncthreads();
+            close_all();
+            seg_cur = tl.seg;
+            __syncthreads();
+        }
+        T row[IT];
+        unsigned br[IT];   // bin << 16 | rank within the tile's bin
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const u64 r = tr.lo + (u64)i * kPassThreads + threadIdx.x;
-            if (r < tr.hi) {
-                const unsigned b = (unsigned)(rhash(R::key(row[i])) >> a.shift) & (F - 1);
-                br[i] = (b << 16) | atomicAdd(&cnt[b], 1u);
-            } else {
+            if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
+                row[i] = R::zero();
                 br[i] = 0xFFFFFFFFu;
+            } else {
+                br[i] = 0u;
             }
         }
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            if (br[i] == 0xFFFFFFFFu) continue;
+            const unsigned b = (unsigned)(rhash(R::key(row[i])) >> a.shift) & (F - 1);
+            br[i] = (b << 16) | atomicAdd(&cnt[b], 1u);
+        }
         __syncthreads();
-        // exclusive scan of the bin counts (first wave, 8 bins per lane) and each
-        // bin's run destination base = scanned global offset - local start
         if (threadIdx.x < 64) {
+            // wave 0: exclusive scan of the bin counts, 8 bins per lane
             const int lane = threadIdx.x;
             unsigned c[8], s = 0;
 #pragma unroll
@@ -342,60 +337,144 @@ __global__ __launch_bounds__(kPassThreads, 4) void k_scatter(PassArgs a) {   // 
                 if (lane >= o) x += y;
             }
             unsigned run = x - s;
-            const u64 hb = (u64)a.tile_start[tr.seg] * F;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const unsigned b = lane * 8 + j;
-                if (b < F) {
-                    cnt[b] = run;
-                    dst_base[b] = (long long)a.hist[hb + (u64)b * tr.ntiles + tr.t] - (long long)run;
-                }
+                if (b < F) start[b] = run;
                 run += c[j];
+            }
+        } else if (threadIdx.x >= kPassThreads - kMaxFan) {
+            // the last 512 threads: fresh buckets for bins whose run overflows
+            // the open one (k of them, one atomic per bin)
+            const unsigned b = threadIdx.x - (kPassThreads - kMaxFan);
+            const unsigned c = b < F ? cnt[b] : 0u;
+            if (c) {
+                const unsigned f = fill[b];
+                const unsigned k = (f + c - 1) >> a.out_pbl;
+                if (k) {
+                    const unsigned nb = atomicAdd(a.nb, k);
+                    const bool fits = (u64)nb + k <= a.max_buckets;
+                    nbase[b] = fits ? nb : kNoBucket;
+                    if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
+                    if (fits) {
+                        const unsigned pid = ((unsigned)tl.seg << a.fbits) | b;
+                        for (unsigned i = 0; i < k; ++i) {
+                            a.bbin[nb + i] = pid;
+                            if (i + 1 < k) a.bfill[nb + i] = PB;
+                        }
+                    }
+                }
             }
         }
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            if (br[i] != 0xFFFFFFFFu) {
-                const unsigned b = br[i] >> 16;
-                const unsigned pos = cnt[b] + (br[i] & 0xffffu);
-                stage[pos] = row[i];
-                sb[pos] = (unsigned short)b;
-            }
+            if (br[i] == 0xFFFFFFFFu) continue;
+            const unsigned b = br[i] >> 16;
+            const unsigned pos = start[b] + (br[i] & 0xffffu);
+            stage[pos] = row[i];
+            sb[pos] = (unsigned short)b;
         }
         __syncthreads();
-        const unsigned n = (unsigned)(tr.hi - tr.lo);
+        const unsigned tn = start[F - 1] + cnt[F - 1];
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
             const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
-            if (j < n) out[(u64)(dst_base[sb[j]] + (long long)j)] = stage[j];
+            if (j >= tn) continue;
+            const unsigned b = sb[j];
+            const unsigned p = fill[b] + (j - start[b]);
+            const unsigned k = p >> a.out_pbl;
+            const unsigned bk = k == 0 ? cur[b] : (nbase[b] == kNoBucket ? kNoBucket : nbase[b] + k - 1);
+            if (bk < a.max_buckets) out[((u64)bk << a.out_pbl) + (p & (PB - 1))] = stage[j];
         }
-        if (!more) break;
-        __syncthreads();   // stage/cnt reused by the next tile
-        wg = wn;
-        tr = tn;
-#pragma unroll
-        for (int i = 0; i < IT; ++i) row[i] = nrow[i];
+        __syncthreads();
+        for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
+            const unsigned c = cnt[b];
+            cnt[b] = 0u;
+            if (!c) continue;
+            const unsigned f = fill[b];
+            const unsigned k = (f + c - 1) >> a.out_pbl;
+            if (k) {
+                cur[b] = nbase[b] == kNoBucket ? kNoBucket : nbase[b] + k - 1;
+                fill[b] = f + c - (k << a.out_pbl);
+            } else {
+                fill[b] = f + c;
+            }
+        }
+        __syncthreads();
     }
+    close_all();
 }
 
-__global__ __launch_bounds__(256) void k_next_off(PassArgs a) {
-    const unsigned F = 1u << a.fbits;
-    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    const u64 tot = (u64)a.nseg * F;
-    if (i < tot) {
-        const int seg = (int)(i >> a.fbits);
-        const unsigned b = (unsigned)(i & (F - 1));
-        const unsigned nt = a.tile_start[seg + 1] - a.tile_start[seg];
-        a.next_off[i] = nt ? a.hist[(u64)a.tile_start[seg] * F + (u64)b * nt] : a.seg_off[seg];
+// Bucket list by partition: count buckets per partition, exclusive scan
+// (k_scan_*), then place every bucket id at its partition's cursor.  Blocks
+// aggregate in LDS first when partitions are few (pass 1: 512).
+constexpr int kListPer = 4;
+constexpr int kListLds = 4096;
+
+__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *nb, u64 *pcnt, int P) {
+    __shared__ unsigned c[kListLds];
+    const unsigned n = *nb;
+    const u64 base = (u64)blockIdx.x * 1024 * kListPer;
+    if (base >= n) return;
+    const bool lds = P <= kListLds;
+    if (lds)
+        for (int i = threadIdx.x; i < P; i += 1024) c[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kListPer; ++i) {
+        const u64 j = base + (u64)i * 1024 + threadIdx.x;
+        if (j < n) {
+            if (lds) atomicAdd(&c[bbin[j]], 1u);
+            else atomicAdd(&pcnt[bbin[j]], 1ull);
+        }
     }
-    if (i == 0) a.next_off[tot] = a.seg_off[a.nseg];
+    if (!lds) return;
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += 1024)
+        if (c[i]) atomicAdd(&pcnt[i], (u64)c[i]);
+}
+
+__global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
+                                                 u64 *pcur, u64 *blist, int P) {
+    __shared__ unsigned c[kListLds];
+    __shared__ u64 cb[kListLds];
+    const unsigned n = *nb;
+    const u64 base = (u64)blockIdx.x * 1024 * kListPer;
+    if (base >= n) return;
+    if (P > kListLds) {
+#pragma unroll
+        for (int i = 0; i < kListPer; ++i) {
+            const u64 j = base + (u64)i * 1024 + threadIdx.x;
+            if (j < n) blist[atomicAdd(&pcur[bbin[j]], 1ull)] = (j << 32) | bfill[j];
+        }
+        return;
+    }
+    for (int i = threadIdx.x; i < P; i += 1024) c[i] = 0u;
+    __syncthreads();
+    unsigned rk[kListPer], bn[kListPer];
+#pragma unroll
+    for (int i = 0; i < kListPer; ++i) {
+        const u64 j = base + (u64)i * 1024 + threadIdx.x;
+        bn[i] = j < n ? bbin[j] : kNoBucket;
+        if (bn[i] != kNoBucket) rk[i] = atomicAdd(&c[bn[i]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += 1024)
+        if (c[i]) cb[i] = atomicAdd(&pcur[i], (u64)c[i]);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kListPer; ++i) {
+        const u64 j = base + (u64)i * 1024 + threadIdx.x;
+        if (bn[i] != kNoBucket) blist[cb[bn[i]] + rk[i]] = (j << 32) | bfill[j];
+    }
 }
 
 // --------------------------------------------------------------- join
 struct JoinArgs {
-    const void *r, *s;               // partitioned packed rows
-    const u64 *r_off, *s_off;        // P + 1 each
+    const void *r, *s;               // final-pass bucket rows
+    const u64 *r_list, *s_list;      // buckets by partition (bucket << 32 | fill), kFinalPbl rows each
+    const u64 *r_pstart, *s_pstart;  // P + 1 each
     int P;
     const unsigned *work_start;      // P + 1: S chunks per partition (0 if no R rows)
     const unsigned *work_owner;      // work item -> partition
@@ -407,42 +486,58 @@ struct JoinArgs {
 };
 
 struct Item {
-    u64 s_lo, s_hi, r_lo, r_hi;
+    u64 s_lo, s_hi, r_lo, r_hi;      // bucket-list positions
 };
 
-template <int CH>
-__device__ __forceinline__ Item item_of(const JoinArgs &a, unsigned w) {
+__device__ __forceinline__ Item item_of(const JoinArgs &a, unsigned w, unsigned chb) {
     const int p = (int)a.work_owner[w];
     const unsigned c = w - a.work_start[p];
     Item it;
-    it.s_lo = a.s_off[p] + (u64)c * CH;
-    const u64 e = a.s_off[p + 1];
-    it.s_hi = it.s_lo + CH < e ? it.s_lo + CH : e;
-    it.r_lo = a.r_off[p];
-    it.r_hi = a.r_off[p + 1];
+    it.s_lo = a.s_pstart[p] + (u64)c * chb;
+    const u64 e = a.s_pstart[p + 1];
+    it.s_hi = it.s_lo + chb < e ? it.s_lo + chb : e;
+    it.r_lo = a.r_pstart[p];
+    it.r_hi = a.r_pstart[p + 1];
     return it;
 }
 
+// Row v of the bucket-list range [lo, hi) (slot v % PB of bucket lo + v/PB);
+// false where the range or the bucket has no such row.
+template <typename T>
+__device__ __forceinline__ bool list_row(const T *rows, const u64 *list, u64 lo, u64 hi, unsigned v, T &out) {
+    constexpr int pbl = kFinalPbl;
+    const u64 li = lo + (v >> pbl);
+    if (li >= hi) return false;
+    const u64 e = list[li];
+    const unsigned off = v & ((1u << pbl) - 1u);
+    if (off >= (unsigned)e) return false;
+    out = rows[((e >> 32) << pbl) + off];
+    return true;
+}
+
 // A persistent workgroup of NT threads walks work items w = wg, wg + grid, ...
-// Work item = (partition, S chunk of up to kJoinSub * NT * SI rows): build
-// the partition's R rows into a 2^TSL-slot LDS table (rounds of RCAP rows
-// for oversized partitions), then probe the chunk in sub-chunks of NT * SI
-// rows.  The next item's first S sub-chunk and R round are loaded into
-// registers before this item's LDS phase.
+// Work item = (partition, chunk of up to kJoinSub * NT * SI / PB S buckets):
+// build the partition's R buckets into a 2^TSL-slot LDS table (rounds of
+// RCAP / PB buckets for oversized partitions), then probe the chunk in
+// sub-chunks of NT * SI / PB buckets.  Requires PB | RCAP
+// and PB | NT * SI (host-checked).
 // ABL (diagnostics only, micro/join_micro.hip; the product uses 0) switches
 // phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build.
-template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0>
+template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems>
 __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per SIMD: <= 128 VGPRs
     typedef Row<WIDE> R;
     typedef typename R::T T;
     typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // output element
     constexpr int TS = 1 << TSL;
     constexpr unsigned kMask = TS - 1;
-    constexpr int SI = kJoinItems;            // S rows per thread per sub-chunk
+    constexpr int SI = SI_;                   // S rows per thread per sub-chunk
     constexpr int RCAP = TS * 5 / 8;          // build rows per round (load factor <= 0.625)
     constexpr int RI = RCAP / NT;             // build rows per thread per round
     constexpr int SUBR = NT * SI;             // rows per sub-chunk
-    constexpr int CH = kJoinSub * SUBR;       // rows per work item
+    constexpr unsigned rb = (unsigned)RCAP >> kFinalPbl;     // buckets per build round
+    constexpr unsigned subb = (unsigned)SUBR >> kFinalPbl;   // buckets per sub-chunk
+    constexpr unsigned chb = (unsigned)kJoinSub * subb;      // buckets per work item
+    static_assert((rb << kFinalPbl) == RCAP && (subb << kFinalPbl) == SUBR, "bucket size must divide rounds");
     // wide: EMPTY key INT64_MIN (rows with that key take the null path);
     // narrow: the all-ones word (row ids < 2^31 never produce it)
     constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
@@ -451,6 +546,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     __shared__ u64 wsum[16];
     __shared__ u64 s_base;
     __shared__ unsigned s_dup;
+    constexpr int NW = NT / 64;
+    __shared__ unsigned s_cw[SI * NW];        // per (row slot, wave) match counts, then offsets
 
     const unsigned total = a.work_start[a.P];
     unsigned w = blockIdx.x;
@@ -460,47 +557,41 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
 
-    Item it = item_of<CH>(a, w);
+    Item it = item_of(a, w, chb);
     T sv_[SI], rv_[RI];
+    unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
+    auto load_r = [&](const Item &x, u64 r0, T *v) {
+        unsigned ok = 0;
+        const u64 r1 = r0 + rb < x.r_hi ? r0 + rb : x.r_hi;
 #pragma unroll
-    for (int i = 0; i < RI; ++i) {
-        const u64 row = it.r_lo + (u64)i * NT + threadIdx.x;
-        rv_[i] = row < it.r_hi ? rrows[row] : R::zero();
-    }
-
-    while (true) {
-        // this item's first S sub-chunk: issued before the table init / build
-        // so its latency hides behind them
+        for (int i = 0; i < RI; ++i) {
+            if (list_row(rrows, a.r_list, r0, r1, (unsigned)(i * NT) + threadIdx.x, v[i])) ok |= 1u << i;
+            else v[i] = R::zero();
+        }
+        return ok;
+    };
+    auto load_s = [&](u64 s0) {
+        unsigned ok = 0;
+        const u64 s1 = s0 + subb < it.s_hi ? s0 + subb : it.s_hi;
 #pragma unroll
         for (int i = 0; i < SI; ++i) {
-            const u64 row = it.s_lo + (u64)i * NT + threadIdx.x;
-            sv_[i] = row < it.s_hi ? srows[row] : R::zero();
+            if (list_row(srows, a.s_list, s0, s1, (unsigned)(i * NT) + threadIdx.x, sv_[i])) ok |= 1u << i;
+            else sv_[i] = R::zero();
         }
-        // ---- prefetch the next work item's build rows
-        const unsigned wn = w + gridDim.x;
-        const bool more = wn < total;
-        Item nx;
-        T nrv[RI];
-        if (more) {
-            nx = item_of<CH>(a, wn);
-#pragma unroll
-            for (int i = 0; i < RI; ++i) {
-                const u64 row = nx.r_lo + (u64)i * NT + threadIdx.x;
-                nrv[i] = row < nx.r_hi ? rrows[row] : R::zero();
-            }
-        }
+        return ok;
+    };
+    while (true) {
+        // this item's first R round and first S sub-chunk: issued before the
+        // table init so their latency hides behind it.  (Prefetching the next
+        // item's R rows instead costs registers -> spills, and measured
+        // slower: profiles/r01_micro_join_buckets.txt.)
+        rok = load_r(it, it.r_lo, rv_);
+        sok = load_s(it.s_lo);
 
         u64 n_null_r = 0;
         bool any_null_s = false;
-        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += RCAP) {
-            const u64 r1 = r0 + RCAP < it.r_hi ? r0 + RCAP : it.r_hi;
-            if (r0 != it.r_lo) {   // later rounds (oversized partitions)
-#pragma unroll
-                for (int i = 0; i < RI; ++i) {
-                    const u64 row = r0 + (u64)i * NT + threadIdx.x;
-                    rv_[i] = row < r1 ? rrows[row] : R::zero();
-                }
-            }
+        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
+            if (r0 != it.r_lo) rok = load_r(it, r0, rv_);   // later rounds (oversized partitions)
             // ---- init: every slot EMPTY (16-B LDS stores)
             for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
             if (threadIdx.x == 0) s_dup = 0u;
@@ -513,9 +604,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             bool act[RI];
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
-                const u64 row = r0 + (u64)i * NT + threadIdx.x;
                 const u64 key = R::key(rv_[i]);
-                act[i] = row < r1;
+                act[i] = (rok >> i) & 1u;
                 if (WIDE && act[i] && key == kEmptyKey64) {
                     ++n_null_r;
                     act[i] = false;
@@ -546,14 +636,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                 __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
             // ---- probe the chunk, one sub-chunk of S rows at a time
-            for (u64 sb = it.s_lo; sb < it.s_hi; sb += SUBR) {
-                if (sb != it.s_lo || r0 != it.r_lo) {
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 row = sb + (u64)i * NT + threadIdx.x;
-                        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
-                    }
-                }
+            for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+                if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
                 // first slot of every row read before any is resolved (SI
                 // independent LDS reads in flight); most rows end there
                 unsigned m[SI], hp[SI];
@@ -563,9 +647,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
 #pragma unroll
                 for (int i = 0; i < SI; ++i) {
                     m[i] = 0xFFFFFFFFu;
-                    const u64 row = sb + (u64)i * NT + threadIdx.x;
                     const u64 key = R::key(sv_[i]);
-                    pa[i] = row < it.s_hi;
+                    pa[i] = (sok >> i) & 1u;
                     if (WIDE && pa[i] && key == kEmptyKey64) {   // matched by the null pass below
                         any_null_s = true;
                         pa[i] = false;
@@ -595,12 +678,65 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                         e = tkey[h];
                     }
                 }
+                if (WRITE && unique) {
+                    // <= 1 match per row: ballot compaction in row-slot-major
+                    // order, so lanes with a match store to consecutive
+                    // addresses (one coalesced run per wave and slot)
+                    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+                    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                    unsigned lpre[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 bal = __ballot(m[i] != 0xFFFFFFFFu);
+                        lpre[i] = (unsigned)__popcll(bal & lt);
+                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                    }
+                    __syncthreads();
+                    if (wv == 0) {   // exclusive scan of the SI * NW run lengths
+                        constexpr int K = (SI * NW + 63) / 64;
+                        unsigned v[K], sum = 0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int j = lane * K + k;
+                            v[k] = j < SI * NW ? s_cw[j] : 0u;
+                            sum += v[k];
+                        }
+                        unsigned x = sum;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const unsigned y = __shfl_up(x, o, 64);
+                            if (lane >= o) x += y;
+                        }
+                        unsigned run = x - sum;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int j = lane * K + k;
+                            if (j < SI * NW) s_cw[j] = run;
+                            run += v[k];
+                        }
+                        if (lane == 63 && x)
+                            s_base = (ABL & 1) ? (u64)w * chb << kFinalPbl : atomicAdd(a.counter, (u64)x);
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if constexpr ((ABL & 2) != 0) break;
+                        if (m[i] == 0xFFFFFFFFu) continue;
+                        const u64 pos = s_base + s_cw[i * NW + wv] + lpre[i];
+                        if (pos < (u64)a.cap) {
+                            orr[pos] = WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull);
+                            oss[pos] = (PT)R::pay(sv_[i]);
+                        }
+                    }
+                    __syncthreads();   // s_cw / s_base reused by the next sub-chunk
+                    continue;
+                }
                 u64 tot;
                 const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
                 if constexpr (!WRITE) {
                     if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
                 } else if (tot) {
-                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * CH : atomicAdd(a.counter, tot);
+                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kFinalPbl : atomicAdd(a.counter, tot);
                     __syncthreads();
                     u64 pos = s_base + pre;
 #pragma unroll
@@ -616,9 +752,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                                 ++pos;
                             }
                         } else {
-                            const u64 row = sb + (u64)i * NT + threadIdx.x;
                             const u64 key = R::key(sv_[i]);
-                            if (row >= it.s_hi || (WIDE && key == kEmptyKey64)) continue;
+                            if (!((sok >> i) & 1u) || (WIDE && key == kEmptyKey64)) continue;
                             unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
                             while (true) {
                                 const u64 e = tkey[h];
@@ -645,18 +780,12 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             if (__syncthreads_or(any_null_s ? 1 : 0)) {
                 u64 nn;
                 (void)block_excl_scan<NT>(n_null_r, wsum, &nn);   // null R rows of this partition
-                for (u64 sb = it.s_lo; sb < it.s_hi; sb += SUBR) {
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 row = sb + (u64)i * NT + threadIdx.x;
-                        sv_[i] = row < it.s_hi ? srows[row] : R::zero();
-                    }
+                for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+                    sok = load_s(sb);
                     u64 cnt = 0;
 #pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 row = sb + (u64)i * NT + threadIdx.x;
-                        if (row < it.s_hi && R::key(sv_[i]) == kEmptyKey64) cnt += nn;
-                    }
+                    for (int i = 0; i < SI; ++i)
+                        if (((sok >> i) & 1u) && R::key(sv_[i]) == kEmptyKey64) cnt += nn;
                     u64 tot;
                     const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
                     if constexpr (!WRITE) {
@@ -666,16 +795,18 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                         __syncthreads();
                         u64 pos = s_base + pre;
                         for (int i = 0; i < SI; ++i) {
-                            const u64 row = sb + (u64)i * NT + threadIdx.x;
-                            if (!(row < it.s_hi && R::key(sv_[i]) == kEmptyKey64)) continue;
-                            for (u64 r = it.r_lo; r < it.r_hi; ++r) {
-                                const T rr = rrows[r];
-                                if (R::key(rr) != kEmptyKey64) continue;
-                                if (pos < (u64)a.cap) {
-                                    orr[pos] = (PT)R::pay(rr);
-                                    oss[pos] = (PT)R::pay(sv_[i]);
+                            if (!(((sok >> i) & 1u) && R::key(sv_[i]) == kEmptyKey64)) continue;
+                            for (u64 li = it.r_lo; li < it.r_hi; ++li) {
+                                const u64 le = a.r_list[li];
+                                for (unsigned o = 0; o < (unsigned)le; ++o) {
+                                    const T rr = rrows[((le >> 32) << kFinalPbl) + o];
+                                    if (R::key(rr) != kEmptyKey64) continue;
+                                    if (pos < (u64)a.cap) {
+                                        orr[pos] = (PT)R::pay(rr);
+                                        oss[pos] = (PT)R::pay(sv_[i]);
+                                    }
+                                    ++pos;
                                 }
-                                ++pos;
                             }
                         }
                         __syncthreads();
@@ -684,11 +815,9 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             }
         }
 
-        if (!more) break;
-        w = wn;
-        it = nx;
-#pragma unroll
-        for (int i = 0; i < RI; ++i) rv_[i] = nrv[i];
+        w += gridDim.x;
+        if (w >= total) break;
+        it = item_of(a, w, chb);
     }
 }
 
@@ -718,6 +847,33 @@ int cu_count() {
 
 inline unsigned blocks_for(u64 n, u64 per) { return (unsigned)((n + per - 1) / per); }
 
+// Workgroups of a partition pass over n rows: one per CU, fewer for small
+// inputs (each open bucket per workgroup and bin is potential slack).
+unsigned pass_grid(u64 n) {
+    const u64 tiles = (n + kTile - 1) / kTile;
+    const u64 g = tiles / 8 > 0 ? tiles / 8 : 1;   // >= 8 tiles per workgroup
+    const u64 cus = (u64)cu_count();
+    return (unsigned)(g < cus ? g : cus);
+}
+
+// Exclusive scan of a u64 array of len elements in place (k_scan_*).
+void scan_u64(u64 *v, u64 len, u64 *sums, hipStream_t st) {
+    const unsigned nb = blocks_for(len, kScanBlock);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, v, len, sums);
+    if (nb > 1) {
+        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, sums, nb);
+        hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, v, len, (const u64 *)sums);
+    }
+}
+
+void chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, unsigned *start, unsigned *owner,
+               u64 *scratch, u64 *sums, hipStream_t st) {
+    const unsigned g = blocks_for((u64)nseg + 1, 256);
+    hipLaunchKernelGGL(k_chunk_count, dim3(g), dim3(256), 0, st, off_a, off_b, nseg, chunk, scratch);
+    scan_u64(scratch, (u64)nseg + 1, sums, st);
+    hipLaunchKernelGGL(k_chunk_finish, dim3(g), dim3(256), 0, st, (const u64 *)scratch, nseg, start, owner);
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- planning
@@ -734,113 +890,139 @@ RadixPlan radix_plan(long long n_build, int force_bits) {
     for (int i = 0; i < pl.passes; ++i) {
         pl.bits[i] = (left + (pl.passes - i) - 1) / (pl.passes - i);
         left -= pl.bits[i];
+        pl.pbl[i] = i == pl.passes - 1 ? kFinalPbl : kPassPbl;
     }
-    for (int i = pl.passes; i < 3; ++i) pl.bits[i] = 0;
+    for (int i = pl.passes; i < 3; ++i) pl.bits[i] = pl.pbl[i] = 0;
     return pl;
 }
 
-size_t radix_hist_elems(long long n, int max_nseg) {
-    return ((size_t)n / kTile + (size_t)max_nseg + 2) * 512;
+// Pass i writes the final set when (passes - 1 - i) is even, else the ping
+// set.  It allocates at most n / PB full buckets plus one open bucket per
+// (workgroup segment run, bin): runs <= G + nseg_in.
+RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
+    RadixNeed need{1, 1};
+    const u64 rows = n > 0 ? (u64)n : 1;
+    u64 nseg = 1;
+    for (int i = 0; i < pl.passes; ++i) {
+        const bool to_final = ((pl.passes - 1 - i) % 2) == 0;
+        const u64 F = 1ull << pl.bits[i];
+        const u64 b = (rows >> pl.pbl[i]) + ((u64)pass_grid(rows) + nseg + 1) * F + 1;
+        if (to_final == final_set) {
+            if (b > need.buckets) need.buckets = b;
+            if ((b << pl.pbl[i]) > need.rows) need.rows = b << pl.pbl[i];
+        }
+        nseg *= F;
+    }
+    return need;
 }
 
-int radix_chunk_rows() { return join_variant().nt * kJoinItems * kJoinSub; }
+unsigned long long radix_tiles(long long n, int max_nseg) {
+    // bucketed tiles: kTile / PB buckets each, <= one partial tile per segment
+    return (u64)(n > 0 ? n : 1) / kTile * 2 + (u64)max_nseg + 2;
+}
 
-// Partition one relation into the plan's 2^total_bits partitions of packed
-// rows (16 B wide, 8 B narrow) in `out`, with partition offsets in out_off
-// (P + 1).  ws.tmp is the ping buffer of multi-pass plans.  Asynchronous; no
-// allocation.
-hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws, void *out,
-                           unsigned long long *out_off, hipStream_t st) {
-    const u64 n = (u64)src.n;
-    hipLaunchKernelGGL(k_set_off, dim3(1), dim3(64), 0, st, ws.off_a, n);
+unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets) {
+    const JoinVariant jv = join_variant();
+    const u64 chb = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kFinalPbl);
+    return s_buckets / chb + (1ull << pl.total_bits) + 2;
+}
+
+// Partition one relation into the plan's 2^total_bits partitions: bucket
+// rows in `out` (with blist / pstart by partition).  ws.tmp is the ping set
+// of multi-pass plans.  Asynchronous; no allocation.
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
+                           const BucketSet &out, hipStream_t st) {
+    const u64 n = (u64)(src.n > 0 ? src.n : 0);
     int nseg = 1;
     int shift = 64;
-    SrcDev in = src;
-    u64 *seg_off = ws.off_a;
-    static const unsigned persist_env = [] {
-        const char *e = getenv("HJ_SCATTER_WG_PER_CU");   // experiments: 0 = one tile per workgroup
-        return e ? (unsigned)atoi(e) : 2u;
-    }();
-    const unsigned persist = persist_env ? persist_env * (unsigned)cu_count() : 0xFFFFFFFFu;
+    const BucketSet *prev = nullptr;
+    int prev_pbl = 0;
+    const unsigned grid = pass_grid(n > 0 ? n : 1);
     for (int pass = 0; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
         shift -= fb;
-        const bool last = pass == pl.passes - 1;
-        // destination: final buffer on the last pass, else alternate so the
-        // last pass lands in `out`
-        void *dst = last ? out : ((((pl.passes - 1 - pass) % 2) == 1) ? ws.tmp : out);
-        u64 *next_off = last ? out_off : (seg_off == ws.off_a ? ws.off_b : ws.off_a);
+        const BucketSet &dst = ((pl.passes - 1 - pass) % 2) == 0 ? out : ws.tmp;
         PassArgs a;
-        a.in = in;
-        a.seg_off = seg_off;
-        a.nseg = nseg;
+        a.in = src;
+        a.n = n;
+        a.in_rows = prev ? prev->rows : nullptr;
+        a.in_list = prev ? prev->blist : nullptr;
+        a.in_pstart = prev ? prev->pstart : nullptr;
+        a.in_pbl = prev_pbl;
         a.tile_start = ws.tile_start;
         a.tile_owner = ws.tile_owner;
-        a.hist = ws.hist;
-        a.out = dst;
-        a.next_off = next_off;
+        a.nseg = nseg;
+        a.out_rows = dst.rows;
+        a.bbin = dst.bbin;
+        a.bfill = dst.bfill;
+        a.nb = ws.nb;
+        {
+            // a write past either array is impossible by the capacity bound
+            // (radix_need); the kernel still clamps to this
+            const u64 by_rows = dst.max_rows >> pl.pbl[pass];
+            a.max_buckets = (unsigned)(by_rows < dst.max_buckets ? by_rows : dst.max_buckets);
+        }
+        a.out_pbl = pl.pbl[pass];
         a.shift = shift;
         a.fbits = fb;
-        const unsigned F = 1u << fb;
-        hipLaunchKernelGGL(k_chunk_map, dim3(1), dim3(1024), 0, st, (const u64 *)seg_off, (const u64 *)nullptr, nseg,
-                           (unsigned)kTile, ws.tile_start);
-        const unsigned grid = (unsigned)(n / kTile + nseg + 1);
-        if (nseg > 1)
-            hipLaunchKernelGGL(k_work_list, dim3(blocks_for((u64)nseg, 256)), dim3(256), 0, st,
-                               (const unsigned *)ws.tile_start, nseg, ws.tile_owner);
-        const u64 hlen = (u64)grid * F;
-        hipError_t e = hipMemsetAsync(ws.hist, 0, hlen * sizeof(u64), st);
+        hipError_t e = hipMemsetAsync(ws.nb, 0, sizeof(unsigned), st);
         if (e != hipSuccess) return e;
-        const unsigned sgrid = grid < persist ? grid : persist;
-#define HJ_PASS(W, FORM)                                                                                  \
-    do {                                                                                                  \
-        hipLaunchKernelGGL((k_hist<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a);                  \
-        const unsigned nb = blocks_for(hlen, kScanBlock);                                                 \
-        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, ws.hist, hlen, ws.scan_sums);      \
-        if (nb > 1) {                                                                                     \
-            hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, ws.scan_sums, nb);                \
-            hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, ws.hist, hlen,                    \
-                               (const u64 *)ws.scan_sums);                                                \
-        }                                                                                                 \
-        hipLaunchKernelGGL((k_scatter<W, FORM>), dim3(sgrid), dim3(kPassThreads), 0, st, a);              \
-    } while (0)
-        if (wide) {
-            if (in.form == kCols64) HJ_PASS(true, kCols64);
-            else HJ_PASS(true, kPackedRow);   // kPacked64 input == packed row layout
-        } else {
-            if (in.form == kCol32) HJ_PASS(false, kCol32);
-            else HJ_PASS(false, kPackedRow);
+        if (prev) {
+            // tiles of kTile / PB buckets per segment, and tile -> segment
+            chunk_map(prev->pstart, nullptr, nseg, (unsigned)(kTile >> prev_pbl), ws.tile_start, ws.tile_owner, ws.pcur,
+                      ws.scan_sums, st);
         }
+        if (n > 0) {
+#define HJ_PASS(W, FORM) hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
+            if (prev) {
+                if (wide) HJ_PASS(true, kBucketed);
+                else HJ_PASS(false, kBucketed);
+            } else if (wide) {
+                if (src.form == kCols64) HJ_PASS(true, kCols64);
+                else HJ_PASS(true, kPackedRow);   // kPacked64 input == packed row layout
+            } else {
+                if (src.form == kCol32) HJ_PASS(false, kCol32);
+                else HJ_PASS(false, kPackedRow);
+            }
 #undef HJ_PASS
-        hipLaunchKernelGGL(k_next_off, dim3(blocks_for((u64)nseg * F + 1, 256)), dim3(256), 0, st, a);
+        }
+        // list the buckets by partition: pstart = scan of per-partition counts
+        const u64 P = (u64)nseg << fb;
+        e = hipMemsetAsync(dst.pstart, 0, (P + 1) * sizeof(u64), st);
+        if (e != hipSuccess) return e;
+        const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
+        hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin, (const unsigned *)ws.nb,
+                           dst.pstart, (int)P);
+        scan_u64(dst.pstart, P + 1, ws.scan_sums, st);
+        e = hipMemcpyAsync(ws.pcur, dst.pstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, ws.pcur, dst.blist, (int)P);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
-        // the next pass reads this pass's packed rows
-        in.key = dst;
-        in.pay = nullptr;
-        in.form = kPackedRow;
-        seg_off = next_off;
-        nseg *= (int)F;
+        prev = &dst;
+        prev_pbl = pl.pbl[pass];
+        nseg = (int)P;
     }
     return hipSuccess;
 }
 
-hipError_t radix_join(bool wide, const RadixPlan &pl, const void *r_rows, const unsigned long long *r_off,
-                      const void *s_rows, const unsigned long long *s_off, long long n_s, unsigned *work_start,
-                      void *out_r, void *out_s, long long cap, unsigned long long *counter,
-                      unsigned long long *dup_flag, bool count_only, hipStream_t st) {
+hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
+                      unsigned s_buckets, unsigned *work_start, void *out_r, void *out_s, long long cap,
+                      unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     const JoinVariant jv = join_variant();
-    const unsigned chunk = (unsigned)(jv.nt * kJoinItems * kJoinSub);
-    hipLaunchKernelGGL(k_chunk_map, dim3(1), dim3(1024), 0, st, s_off, r_off, P, chunk, work_start);
-    hipLaunchKernelGGL(k_work_list, dim3(blocks_for((u64)P, 256)), dim3(256), 0, st, (const unsigned *)work_start, P,
-                       work_owner);
+    if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
+    const unsigned chb = (unsigned)kJoinSub * (unsigned)((jv.nt * kJoinItems) >> kFinalPbl);
+    chunk_map(s.pstart, r.pstart, P, chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     JoinArgs a;
-    a.r = r_rows;
-    a.s = s_rows;
-    a.r_off = r_off;
-    a.s_off = s_off;
+    a.r = r.rows;
+    a.s = s.rows;
+    a.r_list = r.blist;
+    a.s_list = s.blist;
+    a.r_pstart = r.pstart;
+    a.s_pstart = s.pstart;
     a.P = P;
     a.work_start = work_start;
     a.work_owner = work_owner;
@@ -850,7 +1032,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const void *r_rows, const 
     a.cap = cap;
     a.counter = counter;
     a.dup_flag = dup_flag;
-    const unsigned items = (unsigned)((u64)n_s / chunk + (u64)P + 1);
+    const unsigned items = (unsigned)((u64)s_buckets / chb + (u64)P + 1);
     // persistent grid: as many workgroups as fit at once (LDS-limited)
     const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
     const unsigned pg = (unsigned)(per_cu * cu_count());

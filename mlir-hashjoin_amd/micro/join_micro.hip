@@ -1,11 +1,13 @@
-// join_micro.hip -- ablation of the radix join kernel (k_join) on synthetic,
-// already-partitioned PK-FK data: 2^17 partitions x 2048 R rows and 2048 S
-// rows (the C3 shape after partitioning).  ABL bits switch phases off:
-// 1 cursor atomic, 2 output writes, 4 probe, 8 build.
-// Build: hipcc --offload-arch=gfx950 -O3 -I../csrc -I../../include -o join_micro join_micro.hip
+// join_micro.hip -- ablation of the radix join kernel (k_join) on the real
+// partition layout: |R| = |S| = 2^28 PK-FK rows are partitioned by the
+// product's radix_partition (bucket sets), then only the join is timed.
+// ABL bits switch phases off: 1 cursor atomic, 2 output writes, 4 probe,
+// 8 build.  Also reports the bucket-fill statistics of the final sets.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../csrc -I../../include -o join_micro join_micro.hip
 #include "../csrc/hj_radix.hip"
 
 #include <cstdio>
+#include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace hj;
@@ -17,58 +19,123 @@ __device__ u64 mixd(u64 z) {
     return z ^ (z >> 31);
 }
 
-__global__ void k_gen(ulonglong2 *r, ulonglong2 *s, u64 per, int bits, u64 ginv, u64 n) {
+__global__ void k_gen(ulonglong2 *r, ulonglong2 *s, u64 n) {
     u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    u64 p = i / per;
-    u64 h = (p << (64 - bits)) | (mixd(i) >> bits);
-    r[i] = make_ulonglong2(h * ginv, i);
-    u64 j = p * per + mixd(i ^ 0xabcdef) % per;
-    u64 hj = (p << (64 - bits)) | (mixd(j) >> bits);
-    s[i] = make_ulonglong2(hj * ginv, i);
+    r[i] = make_ulonglong2(mixd(i), i);
+    const u64 j = mixd(i ^ 0xabcdef) % n;
+    s[i] = make_ulonglong2(mixd(j), i);
 }
 
-__global__ void k_maps(u64 *r_off, u64 *s_off, unsigned *ws, unsigned *wo, u64 per, int P) {
-    int p = blockIdx.x * 256 + threadIdx.x;
-    if (p > P) return;
-    r_off[p] = (u64)p * per;
-    s_off[p] = (u64)p * per;
-    ws[p] = p;
-    if (p < P) wo[p] = p;
+template <typename T>
+T *dalloc(u64 n) {
+    T *p;
+    CK(hipMalloc(&p, n * sizeof(T) + 16));
+    return p;
+}
+
+BucketSet make_set(RadixNeed nd, int P) {
+    BucketSet b;
+    b.rows = dalloc<ulonglong2>(nd.rows);
+    b.bbin = dalloc<unsigned>(nd.buckets);
+    b.bfill = dalloc<unsigned>(nd.buckets);
+    b.blist = dalloc<u64>(nd.buckets);
+    b.pstart = dalloc<u64>((u64)P + 1);
+    b.max_buckets = (unsigned)nd.buckets;
+    b.max_rows = nd.rows;
+    return b;
 }
 
 int main() {
-    const int bits = 17, P = 1 << bits;
-    const u64 per = 2048, n = (u64)P * per;
-    u64 ginv = 0x9E3779B97F4A7C15ull;
-    for (int i = 0; i < 6; ++i) ginv *= 2 - 0x9E3779B97F4A7C15ull * ginv;
-    ulonglong2 *r, *s;
-    u64 *r_off, *s_off, *out_r, *out_s, *cnt, *dup;
-    unsigned *ws, *wo;
-    CK(hipMalloc(&r, n * 16)); CK(hipMalloc(&s, n * 16));
-    CK(hipMalloc(&r_off, (P + 1) * 8)); CK(hipMalloc(&s_off, (P + 1) * 8));
-    CK(hipMalloc(&ws, (P + 1) * 4)); CK(hipMalloc(&wo, P * 4));
-    CK(hipMalloc(&out_r, n * 8)); CK(hipMalloc(&out_s, n * 8)); CK(hipMalloc(&cnt, 64)); CK(hipMalloc(&dup, 64));
-    hipLaunchKernelGGL(k_gen, dim3(n / 256), dim3(256), 0, 0, r, s, per, bits, ginv, n);
-    hipLaunchKernelGGL(k_maps, dim3(P / 256 + 1), dim3(256), 0, 0, r_off, s_off, ws, wo, per, P);
+    const u64 n = 1ull << 28;
+    ulonglong2 *r = dalloc<ulonglong2>(n), *s = dalloc<ulonglong2>(n);
+    hipLaunchKernelGGL(k_gen, dim3(n / 256), dim3(256), 0, 0, r, s, n);
+    const RadixPlan pl = radix_plan((long long)n);
+    const int P = 1 << pl.total_bits;
+    printf("plan: %d passes, bits %d/%d/%d, P=%d\n", pl.passes, pl.bits[0], pl.bits[1], pl.bits[2], P);
+    RadixWork ws;
+    ws.tmp = make_set(radix_need((long long)n, pl, false), P);
+    ws.nb = dalloc<unsigned>(4);
+    ws.pcur = dalloc<u64>(P + 1);
+    ws.tile_start = dalloc<unsigned>(P + 1);
+    ws.tile_owner = dalloc<unsigned>(radix_tiles((long long)n, P));
+    ws.scan_sums = dalloc<u64>(P / 8192 + 2);
+    const RadixNeed nd = radix_need((long long)n, pl, true);
+    BucketSet rs = make_set(nd, P), ss = make_set(nd, P);
+    SrcDev src;
+    src.form = kPacked64;
+    src.pay = nullptr;
+    src.row_base = 0;
+    src.n = (long long)n;
+    src.key = r;
+    CK(radix_partition(src, true, pl, ws, rs, 0));
+    src.key = s;
+    CK(radix_partition(src, true, pl, ws, ss, 0));
     CK(hipDeviceSynchronize());
-    JoinArgs a;
-    a.r = r; a.s = s; a.r_off = r_off; a.s_off = s_off; a.P = P; a.work_start = ws; a.work_owner = wo;
-    a.tshift = 64 - bits - 12; a.out_r = out_r; a.out_s = out_s; a.cap = (long long)n; a.counter = cnt; a.dup_flag = dup;
+    // fill statistics
+    for (int side = 0; side < 2; ++side) {
+        const BucketSet &b = side ? ss : rs;
+        std::vector<u64> ps(P + 1);
+        CK(hipMemcpy(ps.data(), b.pstart, (P + 1) * 8, hipMemcpyDeviceToHost));
+        std::vector<u64> lst(ps[P]);
+        CK(hipMemcpy(lst.data(), b.blist, ps[P] * 8, hipMemcpyDeviceToHost));
+        u64 rows = 0, part = 0, maxb = 0, over8 = 0, over10 = 0, maxrows = 0;
+        for (int p = 0; p < P; ++p) {
+            u64 pr = 0;
+            for (u64 i = ps[p]; i < ps[p + 1]; ++i) {
+                const unsigned f = (unsigned)lst[i];
+                pr += f;
+                part += f < 256;
+            }
+            rows += pr;
+            const u64 nbk = ps[p + 1] - ps[p];
+            maxb = nbk > maxb ? nbk : maxb;
+            maxrows = pr > maxrows ? pr : maxrows;
+            over8 += nbk > 8;
+            over10 += nbk > 10;
+        }
+        printf("%s: buckets %llu rows %llu partial %llu (%.2f/partition) max buckets %llu max rows %llu  >8 bk %.1f%%  >10 bk %.1f%%\n",
+               side ? "S" : "R", ps[P], rows, part, (double)part / P, maxb, maxrows, 100.0 * over8 / P, 100.0 * over10 / P);
+    }
+    unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_buckets));
+    u64 *out_r = dalloc<u64>(n + (1 << 20)), *out_s = dalloc<u64>(n + (1 << 20)), *cnt = dalloc<u64>(8),
+        *dup = dalloc<u64>(8);
     hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    const int cus = cu_count();
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    // the product launch, then hand-rolled ablation launches with the same args
     auto run = [&](const char *name, auto launch) {
-        CK(hipMemset(cnt, 0, 8)); launch(); CK(hipDeviceSynchronize());
-        u64 m = 0; CK(hipMemcpy(&m, cnt, 8, hipMemcpyDeviceToHost));
+        CK(hipMemset(cnt, 0, 8));
+        launch();
+        CK(hipDeviceSynchronize());
+        u64 m = 0;
+        CK(hipMemcpy(&m, cnt, 8, hipMemcpyDeviceToHost));
         CK(hipEventRecord(e0));
-        for (int i = 0; i < 5; ++i) { CK(hipMemsetAsync(cnt, 0, 8)); launch(); }
-        CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= 5;
+        for (int i = 0; i < 5; ++i) {
+            CK(hipMemsetAsync(cnt, 0, 8));
+            launch();
+        }
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= 5;
         printf("%-34s %7.3f ms  %7.1f GB/s  M=%llu\n", name, ms, (3.0 * n * 16) / ms / 1e6, m);
     };
-#define J(TSL, NT, PER_CU, WR, ABL, NAME)                                                                       \
-    run(NAME, [&] { hipLaunchKernelGGL((k_join<true, WR, TSL, NT, ABL>), dim3(PER_CU * cus), dim3(NT), 0, 0, a); })
+    run("radix_join (product)", [&] {
+        CK(radix_join(true, pl, ws, rs, ss, ss.max_buckets, work, out_r, out_s, (long long)n, cnt, dup, false, 0));
+    });
+    // work map of the product call stays in `work`
+    JoinArgs a;
+    a.r = rs.rows; a.s = ss.rows; a.r_list = rs.blist; a.s_list = ss.blist; a.r_pstart = rs.pstart;
+    a.s_pstart = ss.pstart; a.P = P; a.work_start = work; a.work_owner = work + P + 1;
+    a.out_r = out_r; a.out_s = out_s; a.cap = (long long)n; a.counter = cnt; a.dup_flag = dup;
+    const int cus = cu_count();
+#define J(TSL, NT, PER_CU, WR, ABL, NAME)                                                                  \
+    run(NAME, [&] {                                                                                       \
+        a.tshift = 64 - pl.total_bits - TSL;                                                              \
+        hipLaunchKernelGGL((k_join<true, WR, TSL, NT, ABL>), dim3(PER_CU * cus), dim3(NT), 0, 0, a);      \
+    })
     J(12, 512, 2, true, 0, "full");
     J(12, 512, 2, false, 0, "count only");
     J(12, 512, 2, true, 1, "no atomic");
@@ -76,12 +143,5 @@ int main() {
     J(12, 512, 2, true, 3, "no atomic, no writes");
     J(12, 512, 2, true, 7, "no probe/atomic/writes");
     J(12, 512, 2, true, 15, "loads + init only");
-    J(12, 512, 3, true, 0, "full, 3 WG/CU grid");
-    J(12, 512, 4, true, 0, "full, 4 WG/CU grid (non-resident)");
-    a.tshift = 64 - bits - 11;
-    J(11, 256, 4, true, 0, "tsl11 full (4 WG/CU)");
-    J(11, 256, 4, true, 15, "tsl11 loads + init only");
-    a.tshift = 64 - bits - 13;
-    J(13, 1024, 1, true, 0, "tsl13 full (1 WG/CU)");
     return 0;
 }
