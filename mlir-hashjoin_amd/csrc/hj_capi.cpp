@@ -111,7 +111,7 @@ struct hj_ctx {
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
-    Buf nb, pcur, tile_start, tile_owner, work_start, scan_sums;
+    Buf nb, pcur, tile_start, tile_owner, work_start, work_desc, scan_sums;
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -233,7 +233,9 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
     HJ_TRY(ensure_buf(c->tile_owner, (size_t)hj::radix_tiles(n, (int)P) * 4));
     // work map: P + 1 chunk starts, then the item -> partition owner list
-    HJ_TRY(ensure_buf(c->work_start, (P + 1 + (size_t)hj::radix_join_items(pl, fin.max_buckets)) * 4));
+    const size_t items = (size_t)hj::radix_join_items(pl, fin.max_buckets);
+    HJ_TRY(ensure_buf(c->work_start, (P + 1 + items) * 4));
+    HJ_TRY(ensure_buf(c->work_desc, items * hj::radix_item_desc_bytes()));
     HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
     return HJ_OK;
 }
@@ -313,7 +315,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
         HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_buckets,
-                              (unsigned *)c->work_start.p, out_r, out_s, count_only ? 0 : cap,
+                              (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
                               (unsigned long long *)d_count, c->meta + 1, count_only, st));
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
@@ -608,7 +610,8 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->scan_sums}) free_buf(*b);
+    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums})
+        free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
     {

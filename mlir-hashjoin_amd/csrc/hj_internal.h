@@ -114,8 +114,10 @@ unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_bu
 // Partitioned rows are packed: 16 B {key, pay} (wide) or 8 B key << 32 | row id (narrow).
 hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
                            const BucketSet &out, hipStream_t st);
+size_t radix_item_desc_bytes();
+// work_start: >= P + 1 + radix_join_items words; desc: >= radix_join_items * radix_item_desc_bytes()
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
-                      unsigned s_buckets, unsigned *work_start, void *out_r, void *out_s, long long cap,
+                      unsigned s_buckets, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st);
 
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,

@@ -196,12 +196,12 @@ __global__ __launch_bounds__(1024) void k_scan_add(u64 *a, u64 n, const u64 *sum
 struct PassArgs {
     SrcDev in;                   // pass-1 source (FORM != kBucketed)
     u64 n;                       // pass-1 source rows
+    bool cols_aligned;           // kCols64: both columns 16-B aligned
     // FORM == kBucketed: the previous pass's set, tiles of up to kTile rows
-    // (kTile >> in_pbl buckets) that never straddle two segments
+    // (kTile >> kPassPbl buckets) that never straddle two segments
     const void *in_rows;
     const u64 *in_list;          // bucket << 32 | fill
     const u64 *in_pstart;
-    int in_pbl;
     const unsigned *tile_start;  // nseg + 1
     const unsigned *tile_owner;  // tile -> segment
     int nseg;
@@ -230,7 +230,7 @@ __device__ __forceinline__ PassTile pass_tile(const PassArgs &a, unsigned t) {
     PassTile r;
     if constexpr (FORM == kBucketed) {
         r.seg = a.nseg == 1 ? 0 : (int)a.tile_owner[t];
-        const unsigned bpt = (unsigned)kTile >> a.in_pbl;
+        const unsigned bpt = (unsigned)kTile >> kPassPbl;
         r.lo = a.in_pstart[r.seg] + (u64)(t - a.tile_start[r.seg]) * bpt;
         const u64 e = a.in_pstart[r.seg + 1];
         r.hi = r.lo + bpt < e ? r.lo + bpt : e;
@@ -247,12 +247,15 @@ template <bool WIDE, int FORM>
 __device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, unsigned v, typename Row<WIDE>::T &out) {
     typedef Row<WIDE> R;
     if constexpr (FORM == kBucketed) {
-        const u64 li = t.lo + (v >> a.in_pbl);
+        // input buckets are kPassPbl rows and a wave's 64 lanes share one:
+        // the list entry is wave-uniform (scalar load, SGPRs)
+        static_assert((kPassThreads >> kPassPbl) >= 1, "a wave must stay inside one bucket");
+        const u64 li = t.lo + __builtin_amdgcn_readfirstlane(v >> kPassPbl);
         if (li >= t.hi) return false;
         const u64 e = a.in_list[li];
-        const unsigned off = v & ((1u << a.in_pbl) - 1u);
+        const unsigned off = v & ((1u << kPassPbl) - 1u);
         if (off >= (unsigned)e) return false;
-        out = ((const typename R::T *)a.in_rows)[((e >> 32) << a.in_pbl) + off];
+        out = ((const typename R::T *)a.in_rows)[((e >> 32) << kPassPbl) + off];
         return true;
     } else {
         const u64 row = t.lo + v;
@@ -304,13 +307,36 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         T row[IT];
         unsigned br[IT];   // bin << 16 | rank within the tile's bin
+        if constexpr (WIDE && FORM == kCols64) {
+            // two consecutive rows per lane: one 16-B load from each column
+            // (rows lo + 2 * (i * NT + t) + {0, 1}; order inside a tile is free)
+            const u64 *kc = (const u64 *)a.in.key, *pc = (const u64 *)a.in.pay;
 #pragma unroll
-        for (int i = 0; i < IT; ++i) {
-            if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
-                row[i] = R::zero();
-                br[i] = 0xFFFFFFFFu;
-            } else {
-                br[i] = 0u;
+            for (int i = 0; i < IT / 2; ++i) {
+                const u64 r = tl.lo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
+                if (a.cols_aligned && r + 1 < tl.hi) {
+                    const ulonglong2 k2 = *(const ulonglong2 *)(kc + r);
+                    const ulonglong2 p2 = *(const ulonglong2 *)(pc + r);
+                    row[2 * i] = R::make(k2.x, p2.x);
+                    row[2 * i + 1] = R::make(k2.y, p2.y);
+                    br[2 * i] = br[2 * i + 1] = 0u;
+                } else {
+                    const bool v0 = r < tl.hi, v1 = r + 1 < tl.hi;
+                    row[2 * i] = v0 ? R::make(kc[r], pc[r]) : R::zero();
+                    row[2 * i + 1] = v1 ? R::make(kc[r + 1], pc[r + 1]) : R::zero();
+                    br[2 * i] = v0 ? 0u : 0xFFFFFFFFu;
+                    br[2 * i + 1] = v1 ? 0u : 0xFFFFFFFFu;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < IT; ++i) {
+                if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
+                    row[i] = R::zero();
+                    br[i] = 0xFFFFFFFFu;
+                } else {
+                    br[i] = 0u;
+                }
             }
         }
 #pragma unroll
@@ -477,7 +503,7 @@ struct JoinArgs {
     const u64 *r_pstart, *s_pstart;  // P + 1 each
     int P;
     const unsigned *work_start;      // P + 1: S chunks per partition (0 if no R rows)
-    const unsigned *work_owner;      // work item -> partition
+    const struct ItemDesc *desc;     // per work item (k_item_desc)
     int tshift;                      // LDS slot = (hash >> tshift) & (slots - 1)
     void *out_r, *out_s;
     long long cap;
@@ -485,34 +511,26 @@ struct JoinArgs {
     u64 *dup_flag;                   // set to 1 if any partition's build rows repeat a key
 };
 
-struct Item {
-    u64 s_lo, s_hi, r_lo, r_hi;      // bucket-list positions
+struct ItemDesc {
+    u64 s_lo, s_hi, r_lo, r_hi;      // bucket-list positions of the item's S chunk / the partition's R
 };
 
-__device__ __forceinline__ Item item_of(const JoinArgs &a, unsigned w, unsigned chb) {
-    const int p = (int)a.work_owner[w];
-    const unsigned c = w - a.work_start[p];
-    Item it;
-    it.s_lo = a.s_pstart[p] + (u64)c * chb;
-    const u64 e = a.s_pstart[p + 1];
-    it.s_hi = it.s_lo + chb < e ? it.s_lo + chb : e;
-    it.r_lo = a.r_pstart[p];
-    it.r_hi = a.r_pstart[p + 1];
-    return it;
-}
-
-// Row v of the bucket-list range [lo, hi) (slot v % PB of bucket lo + v/PB);
-// false where the range or the bucket has no such row.
-template <typename T>
-__device__ __forceinline__ bool list_row(const T *rows, const u64 *list, u64 lo, u64 hi, unsigned v, T &out) {
-    constexpr int pbl = kFinalPbl;
-    const u64 li = lo + (v >> pbl);
-    if (li >= hi) return false;
-    const u64 e = list[li];
-    const unsigned off = v & ((1u << pbl) - 1u);
-    if (off >= (unsigned)e) return false;
-    out = rows[((e >> 32) << pbl) + off];
-    return true;
+// One descriptor per work item, so the join reads its item with one
+// (scalar) load instead of the owner -> partition -> offsets chain.
+__global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
+                                                   const u64 *s_pstart, const u64 *r_pstart, int P, unsigned chb,
+                                                   ItemDesc *desc) {
+    const unsigned w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= work_start[P]) return;
+    const int p = (int)work_owner[w];
+    const unsigned c = w - work_start[p];
+    ItemDesc d;
+    d.s_lo = s_pstart[p] + (u64)c * chb;
+    const u64 e = s_pstart[p + 1];
+    d.s_hi = d.s_lo + chb < e ? d.s_lo + chb : e;
+    d.r_lo = r_pstart[p];
+    d.r_hi = r_pstart[p + 1];
+    desc[w] = d;
 }
 
 // A persistent workgroup of NT threads walks work items w = wg, wg + grid, ...
@@ -557,41 +575,71 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
 
-    Item it = item_of(a, w, chb);
-    T sv_[SI], rv_[RI];
-    unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
-    auto load_r = [&](const Item &x, u64 r0, T *v) {
-        unsigned ok = 0;
-        const u64 r1 = r0 + rb < x.r_hi ? r0 + rb : x.r_hi;
+    // Row slot i of thread t is row (t % PB) of bucket lo + i * G + t / PB
+    // (G = NT / PB buckets per slot): a wave's 64 lanes share the bucket, so
+    // list entries are wave-uniform (scalar loads into SGPRs) and can be
+    // fetched one item ahead without costing VGPRs.
+    constexpr unsigned G = NT >> kFinalPbl;
+    static_assert((G << kFinalPbl) == NT, "workgroup must span whole buckets");
+    const unsigned hb = __builtin_amdgcn_readfirstlane(threadIdx.x >> kFinalPbl);
+    const unsigned off = threadIdx.x & ((1u << kFinalPbl) - 1u);
+    // list entries (bucket << 32 | fill; 0 = none) of positions [lo, min(lo + n*G, hi))
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
 #pragma unroll
-        for (int i = 0; i < RI; ++i) {
-            if (list_row(rrows, a.r_list, r0, r1, (unsigned)(i * NT) + threadIdx.x, v[i])) ok |= 1u << i;
-            else v[i] = R::zero();
+        for (int i = 0; i < n; ++i) {
+            const u64 li = lo + (u64)i * G + hb;
+            e[i] = li < hi ? list[li] : 0ull;
+        }
+    };
+    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
+        unsigned ok = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            if (off < (unsigned)e[i]) {
+                v[i] = rows[((e[i] >> 32) << kFinalPbl) + off];
+                ok |= 1u << i;
+            } else {
+                v[i] = R::zero();
+            }
         }
         return ok;
     };
+    T sv_[SI], rv_[RI];
+    unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
+    u64 er[RI], es[SI];
+    ItemDesc it = a.desc[w];
+    ents(a.r_list, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
+    ents(a.s_list, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    ItemDesc nx = a.desc[w + gridDim.x < total ? w + gridDim.x : w];
+    auto load_r = [&](u64 r0) {
+        ents(a.r_list, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
+        return rows_of(rrows, er, rv_, RI);
+    };
     auto load_s = [&](u64 s0) {
-        unsigned ok = 0;
-        const u64 s1 = s0 + subb < it.s_hi ? s0 + subb : it.s_hi;
-#pragma unroll
-        for (int i = 0; i < SI; ++i) {
-            if (list_row(srows, a.s_list, s0, s1, (unsigned)(i * NT) + threadIdx.x, sv_[i])) ok |= 1u << i;
-            else sv_[i] = R::zero();
-        }
-        return ok;
+        ents(a.s_list, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
+        return rows_of(srows, es, sv_, SI);
     };
     while (true) {
         // this item's first R round and first S sub-chunk: issued before the
         // table init so their latency hides behind it.  (Prefetching the next
-        // item's R rows instead costs registers -> spills, and measured
-        // slower: profiles/r01_micro_join_buckets.txt.)
-        rok = load_r(it, it.r_lo, rv_);
-        sok = load_s(it.s_lo);
+        // item's R rows instead costs VGPRs -> spills, and measured slower:
+        // profiles/r01_micro_join_buckets.txt; its list entries and the
+        // descriptor after it are prefetched instead.)
+        rok = rows_of(rrows, er, rv_, RI);
+        sok = rows_of(srows, es, sv_, SI);
+        const bool more = w + gridDim.x < total;
+        u64 ner[RI], nes[SI];
+        ItemDesc nnx = nx;
+        if (more) {
+            ents(a.r_list, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
+            ents(a.s_list, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+            if (w + 2 * gridDim.x < total) nnx = a.desc[w + 2 * gridDim.x];
+        }
 
         u64 n_null_r = 0;
         bool any_null_s = false;
         for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
-            if (r0 != it.r_lo) rok = load_r(it, r0, rv_);   // later rounds (oversized partitions)
+            if (r0 != it.r_lo) rok = load_r(r0);   // later rounds (oversized partitions)
             // ---- init: every slot EMPTY (16-B LDS stores)
             for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
             if (threadIdx.x == 0) s_dup = 0u;
@@ -815,9 +863,14 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             }
         }
 
+        if (!more) break;
         w += gridDim.x;
-        if (w >= total) break;
-        it = item_of(a, w, chb);
+        it = nx;
+        nx = nnx;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) er[i] = ner[i];
+#pragma unroll
+        for (int i = 0; i < SI; ++i) es[i] = nes[i];
     }
 }
 
@@ -921,6 +974,8 @@ unsigned long long radix_tiles(long long n, int max_nseg) {
     return (u64)(n > 0 ? n : 1) / kTile * 2 + (u64)max_nseg + 2;
 }
 
+size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
+
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets) {
     const JoinVariant jv = join_variant();
     const u64 chb = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kFinalPbl);
@@ -945,10 +1000,10 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         PassArgs a;
         a.in = src;
         a.n = n;
+        a.cols_aligned = ((((uintptr_t)src.key) | ((uintptr_t)src.pay)) & 15) == 0;
         a.in_rows = prev ? prev->rows : nullptr;
         a.in_list = prev ? prev->blist : nullptr;
         a.in_pstart = prev ? prev->pstart : nullptr;
-        a.in_pbl = prev_pbl;
         a.tile_start = ws.tile_start;
         a.tile_owner = ws.tile_owner;
         a.nseg = nseg;
@@ -969,7 +1024,8 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         if (e != hipSuccess) return e;
         if (prev) {
             // tiles of kTile / PB buckets per segment, and tile -> segment
-            chunk_map(prev->pstart, nullptr, nseg, (unsigned)(kTile >> prev_pbl), ws.tile_start, ws.tile_owner, ws.pcur,
+            if (prev_pbl != kPassPbl) return hipErrorInvalidValue;   // pass inputs are kPassPbl buckets
+            chunk_map(prev->pstart, nullptr, nseg, (unsigned)(kTile >> kPassPbl), ws.tile_start, ws.tile_owner, ws.pcur,
                       ws.scan_sums, st);
         }
         if (n > 0) {
@@ -1008,7 +1064,7 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
 }
 
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
-                      unsigned s_buckets, unsigned *work_start, void *out_r, void *out_s, long long cap,
+                      unsigned s_buckets, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
@@ -1016,6 +1072,10 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
     const unsigned chb = (unsigned)kJoinSub * (unsigned)((jv.nt * kJoinItems) >> kFinalPbl);
     chunk_map(s.pstart, r.pstart, P, chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    const unsigned items = (unsigned)((u64)s_buckets / chb + (u64)P + 1);
+    hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
+                       (const unsigned *)work_owner, (const u64 *)s.pstart, (const u64 *)r.pstart, P, chb,
+                       (ItemDesc *)desc);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -1025,14 +1085,13 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.s_pstart = s.pstart;
     a.P = P;
     a.work_start = work_start;
-    a.work_owner = work_owner;
+    a.desc = (const ItemDesc *)desc;
     a.tshift = 64 - pl.total_bits - jv.tsl;   // the hash bits right below the partition bits
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;
     a.counter = counter;
     a.dup_flag = dup_flag;
-    const unsigned items = (unsigned)((u64)s_buckets / chb + (u64)P + 1);
     // persistent grid: as many workgroups as fit at once (LDS-limited)
     const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
     const unsigned pg = (unsigned)(per_cu * cu_count());

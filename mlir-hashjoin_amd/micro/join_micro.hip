@@ -98,6 +98,7 @@ int main() {
                side ? "S" : "R", ps[P], rows, part, (double)part / P, maxb, maxrows, 100.0 * over8 / P, 100.0 * over10 / P);
     }
     unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_buckets));
+    void *desc = dalloc<char>(radix_join_items(pl, ss.max_buckets) * radix_item_desc_bytes());
     u64 *out_r = dalloc<u64>(n + (1 << 20)), *out_s = dalloc<u64>(n + (1 << 20)), *cnt = dalloc<u64>(8),
         *dup = dalloc<u64>(8);
     hipEvent_t e0, e1;
@@ -123,12 +124,12 @@ int main() {
         printf("%-34s %7.3f ms  %7.1f GB/s  M=%llu\n", name, ms, (3.0 * n * 16) / ms / 1e6, m);
     };
     run("radix_join (product)", [&] {
-        CK(radix_join(true, pl, ws, rs, ss, ss.max_buckets, work, out_r, out_s, (long long)n, cnt, dup, false, 0));
+        CK(radix_join(true, pl, ws, rs, ss, ss.max_buckets, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0));
     });
     // work map of the product call stays in `work`
     JoinArgs a;
     a.r = rs.rows; a.s = ss.rows; a.r_list = rs.blist; a.s_list = ss.blist; a.r_pstart = rs.pstart;
-    a.s_pstart = ss.pstart; a.P = P; a.work_start = work; a.work_owner = work + P + 1;
+    a.s_pstart = ss.pstart; a.P = P; a.work_start = work; a.desc = (const ItemDesc *)desc;
     a.out_r = out_r; a.out_s = out_s; a.cap = (long long)n; a.counter = cnt; a.dup_flag = dup;
     const int cus = cu_count();
 #define J(TSL, NT, PER_CU, WR, ABL, NAME)                                                                  \
