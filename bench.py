@@ -76,16 +76,17 @@ def cpu_baseline(seed, log2n, threads):
                       f"(init {ph[0]:.2f} / build {ph[1]:.2f} / count {ph[2]:.2f} / probe {ph[3]:.2f} s)"}
 
 
-def pmc_traffic(config, n_gpus):
-    """HBM bytes per probe launch from the committed rocprofv3 PMC summary of
-    this workload (profiles/pmc_latest.json), or None."""
+def pmc_traffic(config, n_gpus, kernel):
+    """HBM bytes per launch of `kernel` for this workload from the committed
+    rocprofv3 PMC summary (profiles/pmc_latest.json, written by
+    profiles/pmc_to_json.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get(f"{config}/n{n_gpus}")
-        return None if e is None else e.get("probe_hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        e = d.get(f"{config}/n{n_gpus}", {}).get("kernels", {}).get(kernel)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except (OSError, ValueError, AttributeError):
         return None
 
 
@@ -192,16 +193,23 @@ def main():
     value = NS / (ms / 1000.0)
     ph = {k: round(v / a.steps, 4) for k, v in phases.items() if v > 0}
 
-    # Roofline of the dominant kernel sequence, the probe phase: algorithmic
-    # bytes per launch = |S_local| x (16 B stream S + 16 B one slot read) +
-    # M_local x 16 B output (SURVEY 8(d), 48 B per probe row at f = 1), over
-    # the probe phase's average HIP-event duration on the launch stream.
+    # Roofline of the dominant kernel (DESIGN.md "Measurement").  Radix: k_join,
+    # the longest single launch; algorithmic bytes per launch = 16 B per R row
+    # + 16 B per S row read once + 16 B per output pair (= 48 B per probe row
+    # at |R| = |S|, f = 1).  Global table: k_probe, 16 B S row + 16 B slot +
+    # 16 B output per probe row.  Duration: HIP events on the
+    # launch stream around the join (probe_join phase).
     probe_ms = phases["probe"] / a.steps
-    probe_bytes = ns * 32 + m_local * 16
-    achieved = probe_bytes / (probe_ms / 1000.0) / 1e9 if probe_ms > 0 else None
-    build_ms = (phases["init"] + phases["build"]) / a.steps
     join_ms = phases["probe_join"] / a.steps
+    build_ms = (phases["init"] + phases["build"]) / a.steps
     strategy = hj.strategy_used or a.strategy
+    if strategy == "radix":
+        kern, kbytes = "k_join", (nr + ns) * 16 + m_local * 16
+    else:
+        kern, kbytes = "k_probe", ns * 32 + m_local * 16
+    achieved = kbytes / (join_ms / 1000.0) / 1e9 if join_ms > 0 else None
+    probe_bytes = ns * 32 + m_local * 16   # 48 B per probe row at f = 1
+    passes = hj.radix_passes if strategy == "radix" else 0
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),
@@ -224,26 +232,30 @@ def main():
         "phase_ms": ph,
         "strategy": strategy,
         "roofline": {
-            "kernel": ("probe phase: S radix partition (k_hist+k_scatter per pass) + k_join" if strategy == "radix"
-                       else "k_probe (hj_kernels.hip)"),
+            "kernel": f"{kern} ({'hj_radix.hip' if kern == 'k_join' else 'hj_kernels.hip'})",
             "bound": "hbm",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": pmc_traffic(a.config, world),
-            "algorithmic_bytes_per_launch": probe_bytes,
-            "avg_launch_ms": round(probe_ms, 4),
+            "traffic": pmc_traffic(a.config, world, kern),
+            "algorithmic_bytes_per_launch": kbytes,
+            "avg_launch_ms": round(join_ms, 4),
         },
-        "build_roofline": {
-            "kernel": "R radix partition" if strategy == "radix" else "k_init + k_build",
-            "achieved": round(nr * 32 / (build_ms / 1000.0) / 1e9, 1) if build_ms > 0 else None,
-            "unit": "GB/s", "algorithmic_bytes_per_launch": nr * 32, "avg_launch_ms": round(build_ms, 4),
+        # the whole probe phase (S partition passes + join for radix) at
+        # SURVEY 8(d)'s 48 B per probe row
+        "probe_phase": {
+            "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
+            "frac": round(probe_bytes / (probe_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4) if probe_ms > 0 else None,
+            "unit": "GB/s", "algorithmic_bytes": probe_bytes, "ms": round(probe_ms, 4),
         },
-        "join_kernel": None if strategy != "radix" or join_ms <= 0 else {
-            "kernel": "k_join (hj_radix.hip)", "avg_launch_ms": round(join_ms, 4),
-            "algorithmic_bytes_per_launch": (nr + ns) * 16 + m_local * 16,
-            "achieved": round(((nr + ns) * 16 + m_local * 16) / (join_ms / 1000.0) / 1e9, 1), "unit": "GB/s"},
+        # build phase: radix = R partition passes, each reading and writing 16 B per row
+        "build_phase": {
+            "kernel": f"k_pass x{passes}" if strategy == "radix" else "k_init + k_build",
+            "algorithmic_bytes": nr * 32 * max(1, passes),
+            "achieved": round(nr * 32 * max(1, passes) / (build_ms / 1000.0) / 1e9, 1) if build_ms > 0 else None,
+            "unit": "GB/s", "ms": round(build_ms, 4),
+        },
     }
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
         threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))

@@ -88,6 +88,9 @@ int hj_ctx_strategy_used(const hj_ctx *ctx);
 /* GLOBAL: slot capacity of the table (power of two, >= 2 x build rows);
  * RADIX: number of partitions. */
 int64_t hj_ctx_table_capacity(const hj_ctx *ctx);
+/* RADIX: partition passes of the current build (1..3) and their fan-out bits
+ * (bits[0..passes-1]); returns 0 passes for GLOBAL / no build. */
+int hj_ctx_radix_plan(const hj_ctx *ctx, int *passes, int bits[3]);
 /* 1 if the build side repeats a key, 0 if not (synchronises).  Known after
  * the build (GLOBAL) or after the first probe (RADIX). */
 int hj_ctx_build_has_duplicates(hj_ctx *ctx);

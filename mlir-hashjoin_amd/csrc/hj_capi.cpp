@@ -112,6 +112,7 @@ struct hj_ctx {
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
     Buf nb, pcur, tile_start, tile_owner, work_start, work_desc, scan_sums;
+    Buf slow;   // global-table probe: tiles for the general path
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -329,7 +330,8 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     out.cap = count_only ? 0 : cap;
     out.counter = (unsigned long long *)d_count;
     record(c, kEvProbe0, st);
-    HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, st));
+    HJ_TRY(ensure_buf(c->slow, (hj::probe_tiles(src.n) + 1) * sizeof(unsigned)));
+    HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, (unsigned *)c->slow.p, st));
     record(c, kEvProbe1, st);
     c->rec[2] = c->timing;
     c->rec_mid = false;
@@ -610,7 +612,8 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums})
+    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums,
+                   &c->slow})
         free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -641,6 +644,14 @@ int64_t hj_ctx_table_capacity(const hj_ctx *c) {
     if (!c || c->layout < 0) return 0;
     if (c->used == HJ_STRATEGY_RADIX) return (int64_t)(1ll << c->plan.total_bits);   // partitions
     return (int64_t)(1ll << c->bits);
+}
+
+int hj_ctx_radix_plan(const hj_ctx *c, int *passes, int bits[3]) {
+    if (!c || !passes || !bits) HJ_FAIL(HJ_ERR_ARG, "null argument");
+    const bool radix = c->layout >= 0 && c->used == HJ_STRATEGY_RADIX;
+    *passes = radix ? c->plan.passes : 0;
+    for (int i = 0; i < 3; ++i) bits[i] = radix ? c->plan.bits[i] : 0;
+    return HJ_OK;
 }
 
 int hj_ctx_build_has_duplicates(hj_ctx *c) {

@@ -39,7 +39,7 @@ struct TableDev {
     unsigned long long mask;         // cap - 1
     int shift;                       // 64 - log2(cap)
     unsigned long long *side;        // wide: payloads of INT64_MIN-key rows
-    unsigned long long *meta;        // [0] side count, [1] dup-seen flag, [2..] scratch counters
+    unsigned long long *meta;        // [0] side count, [1] dup-seen flag, [3] slow-tile count, [8..] cursors
 };
 
 enum Layout : int { kWide = 0, kNarrow = 1 };
@@ -65,8 +65,11 @@ struct OutDev {
 // launchers (hipError_t of the launch; all asynchronous on `st`)
 hipError_t launch_init(const TableDev &t, int layout, unsigned long long cap, hipStream_t st);
 hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStream_t st);
+// slow: >= probe_tiles(src.n) words (tiles handed to the general path; the
+// count lives in meta[3])
+size_t probe_tiles(long long n);
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
-                        bool count_only, hipStream_t st);
+                        bool count_only, unsigned *slow, hipStream_t st);
 
 // ---------------------------------------------------------------- radix join
 // (hj_radix.hip) partitions both relations by the top bits of the key hash

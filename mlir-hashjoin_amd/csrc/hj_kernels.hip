@@ -5,9 +5,9 @@
 //   build         join_v1.mlir:213-277  -> k_build   (linear probing, 64-bit CAS)
 //   count         join_v1.mlir:288-425  -> k_probe<WRITE=false>
 //   probe v1/v2   join_v1.mlir:436-521, join_v2.mlir:450-604
-//                                       -> k_probe<WRITE=true>: LDS-staged
-//                                          output block, one global cursor
-//                                          add per block, coalesced flush
+//                                       -> k_probe<WRITE=true>: ILP slot
+//                                          reads, ballot-compacted output,
+//                                          one global cursor add per block
 // plus the radix partition used by the multi-GPU exchange and the
 // counter-based generators of the benchmark inputs.
 //
@@ -21,7 +21,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kBuildItems = 4;   // rows per thread in build (CAS ILP)
-constexpr int kProbeItems = 4;   // rows per thread in probe (tile = 1024 rows)
+constexpr int kProbeItems = 8;   // rows per thread in probe (tile = 2048 rows)
 constexpr int kPartItems = 8;    // rows per thread in partition
 
 __device__ __forceinline__ unsigned long long slot_of(unsigned long long k, int shift) {
@@ -164,42 +164,45 @@ __global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
 }
 
 // ------------------------------------------------------------------ probe
-// count (join_v2.mlir:311-439) and probe (join_v1.mlir:436-521,
-// join_v2.mlir:450-604) in one kernel family.
+// count (join_v1.mlir:288-425, join_v2.mlir:311-439) and probe
+// (join_v1.mlir:436-521, join_v2.mlir:450-604) in one kernel family.
 //
-// Each thread owns kProbeItems rows of a 1024-row tile (coalesced loads,
-// statically indexed registers).  The probe of a lane is one flattened loop:
-// every iteration issues exactly one slot load; when the current row is
-// resolved (EMPTY reached, or matched with a duplicate-free build side) the
-// lane moves to its next row, so the wave runs max(sum of probe lengths)
-// iterations instead of sum(max) -- divergence across rows is absorbed.
+// Each thread owns kProbeItems rows of a 2048-row tile (coalesced loads).
 //
-// Output (WRITE): matches are staged in LDS (the v2 idea, join_v2.mlir:
-// 525-538) through a wave-aggregated LDS cursor; the tile then reserves its
-// range with ONE global 64-bit atomic add and flushes coalesced (8 B/lane per
-// column).  Tiles producing more than 1024 matches spill the excess straight
-// to global through the same cursor (the v2 overflow path, :539-549).  The
-// cursor counts every match, so a caller whose capacity was too small still
-// learns the exact M (rows past cap are dropped).
+// Fast path (duplicate-free build side, no INT64_MIN probe key in the tile):
+// every row's first slot load is issued before any is resolved, so a lane
+// has kProbeItems random reads in flight (the table read is latency-bound:
+// one dependent read per lane at a time left HBM idle); rows still open
+// after their first slot walk the chain.  A row matches at most once, so
+// the output is compacted with wave ballots in row-slot-major order: each
+// store instruction writes one contiguous run per wave, after ONE global
+// cursor add per tile.
+//
+// General path (duplicates or null keys): a flattened per-lane loop (one
+// slot load per iteration; a lane moves to its next row when the current is
+// resolved) with matches staged in LDS through a wave-aggregated cursor (the
+// v2 idea, join_v2.mlir:525-538), one cursor add per tile and a coalesced
+// flush; more than kStage matches spill straight to global (the v2 overflow
+// path, :539-549).  The cursor counts every match, so a caller whose
+// capacity was too small still learns the exact M (rows past cap dropped).
 template <int L, int FORM, bool WRITE>
-__global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out) {
+__global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out, unsigned *slow) {
     using LY = Lay<L>;
     using slot_t = typename LY::slot_t;
     using out_t = typename LY::out_t;
     constexpr int kTile = kBlock * kProbeItems;
-    __shared__ out_t st_r[WRITE ? kTile : 1];
-    __shared__ out_t st_s[WRITE ? kTile : 1];
-    __shared__ unsigned st_n;
+    constexpr int NW = kBlock / 64;
     __shared__ unsigned long long st_base;
-    __shared__ unsigned long long wsum[kBlock / 64];
+    __shared__ unsigned long long wsum[NW];
+    __shared__ unsigned s_cw[kProbeItems * NW];
 
     const slot_t *sl = (const slot_t *)t.slots;
-    if (threadIdx.x == 0) st_n = 0u;
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
 
     const long long base = (long long)blockIdx.x * kTile + threadIdx.x;
     unsigned long long K[kProbeItems], P[kProbeItems];
     bool V[kProbeItems];
+    bool has_null = false;
 #pragma unroll
     for (int i = 0; i < kProbeItems; ++i) {
         const long long row = base + (long long)i * kBlock;
@@ -207,87 +210,201 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
         Tuple tp = V[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
         K[i] = tp.k;
         P[i] = tp.p;
+        has_null |= V[i] && LY::null_key(K[i]);
     }
-    __syncthreads();   // st_n visible
-
-    unsigned long long cnt = 0;
-    auto emit = [&](unsigned long long rv, unsigned long long sv) {
-        if constexpr (!WRITE) {
-            ++cnt;
-        } else {
-            const unsigned idx = atomicAdd(&st_n, 1u);
-            if (idx < (unsigned)kTile) {
-                st_r[idx] = (out_t)rv;
-                st_s[idx] = (out_t)sv;
-            } else {
-                const unsigned long long g = atomicAdd(out.counter, 1ull);
-                if (g < (unsigned long long)out.cap) {
-                    ((out_t *)out.r)[g] = (out_t)rv;
-                    ((out_t *)out.s)[g] = (out_t)sv;
-                }
-            }
-        }
-    };
-
-    int it = -1;
-    bool have = false;
-    unsigned long long k = 0, p = 0, hh = 0;
-    while (true) {
-        while (!have) {
-            if (++it >= kProbeItems) break;
-            if (!pick(V, it)) continue;
-            k = pick(K, it);
-            p = pick(P, it);
-            if (LY::null_key(k)) {   // wide: INT64_MIN probe key matches every side row
-                const unsigned long long ns = t.meta[0];
-                for (unsigned long long j = 0; j < ns; ++j) emit(t.side[j], p);
-                continue;
-            }
-            hh = slot_of(k, t.shift);
-            have = true;
-        }
-        if (!have) break;
-        const slot_t s = sl[hh];
-        if (LY::empty(s)) {
-            have = false;
-        } else {
-            if (LY::key(s) == k) {
-                emit(LY::pay(s), p);
-                if (unique) have = false;
+    if (!unique || __syncthreads_or(has_null ? 1 : 0)) {
+        // general path: k_probe_slow takes this tile
+        if (threadIdx.x == 0) slow[atomicAdd(&t.meta[3], 1ull)] = blockIdx.x;
+        return;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    slot_t S[kProbeItems];
+    unsigned long long H[kProbeItems];
+#pragma unroll
+    for (int i = 0; i < kProbeItems; ++i) {
+        H[i] = slot_of(K[i], t.shift);
+        if (V[i]) S[i] = sl[H[i]];
+    }
+    unsigned found = 0;
+    unsigned long long RP[kProbeItems];
+#pragma unroll
+    for (int i = 0; i < kProbeItems; ++i) {
+        RP[i] = 0;
+        if (!V[i]) continue;
+        slot_t sv = S[i];
+        unsigned long long hh = H[i];
+        while (!LY::empty(sv)) {
+            if (LY::key(sv) == K[i]) {
+                found |= 1u << i;
+                RP[i] = LY::pay(sv);
+                break;
             }
             hh = (hh + 1) & t.mask;
+            sv = sl[hh];
         }
     }
-
-    if constexpr (WRITE) {
-        __syncthreads();
-        const unsigned nb = st_n;
-        const unsigned nl = nb < (unsigned)kTile ? nb : (unsigned)kTile;
-        if (threadIdx.x == 0) st_base = nl ? atomicAdd(out.counter, (unsigned long long)nl) : 0ull;
-        __syncthreads();
-        const unsigned long long gb = st_base;
-        out_t *orr = (out_t *)out.r;
-        out_t *oss = (out_t *)out.s;
-        for (unsigned j = threadIdx.x; j < nl; j += kBlock) {
-            const unsigned long long g = gb + j;
-            if (g < (unsigned long long)out.cap) {
-                orr[g] = st_r[j];
-                oss[g] = st_s[j];
-            }
-        }
-    } else {
-        // block total: wave reduction (64 lanes) then one add per block
-        unsigned long long c = cnt;
+    if constexpr (!WRITE) {
+        unsigned long long c = (unsigned long long)__popc(found);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+        if (lane == 0) wsum[wv] = c;
         __syncthreads();
         if (threadIdx.x == 0) {
             unsigned long long tot = 0;
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) tot += wsum[w];
+            for (int w = 0; w < NW; ++w) tot += wsum[w];
             if (tot) atomicAdd(out.counter, tot);
         }
+    } else {
+        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        unsigned lpre[kProbeItems];
+#pragma unroll
+        for (int i = 0; i < kProbeItems; ++i) {
+            const unsigned long long bal = __ballot((found >> i) & 1u);
+            lpre[i] = (unsigned)__popcll(bal & lt);
+            if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+        }
+        __syncthreads();
+        if (wv == 0) {   // exclusive scan of the kProbeItems * NW runs (<= 64)
+            static_assert(kProbeItems * NW <= 64, "one lane per run");
+            const unsigned v = lane < kProbeItems * NW ? s_cw[lane] : 0u;
+            unsigned x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane < kProbeItems * NW) s_cw[lane] = x - v;
+            if (lane == 63) st_base = x ? atomicAdd(out.counter, (unsigned long long)x) : 0ull;
+        }
+        __syncthreads();
+        out_t *orr = (out_t *)out.r;
+        out_t *oss = (out_t *)out.s;
+#pragma unroll
+        for (int i = 0; i < kProbeItems; ++i) {
+            if (!((found >> i) & 1u)) continue;
+            const unsigned long long g = st_base + s_cw[i * NW + wv] + lpre[i];
+            if (g < (unsigned long long)out.cap) {
+                orr[g] = (out_t)RP[i];
+                oss[g] = (out_t)P[i];
+            }
+        }
+    }
+}
+
+// General path over the tiles k_probe handed over (slow[0 .. meta[3])):
+// persistent workgroups, one tile at a time.
+template <int L, int FORM, bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, OutDev out, const unsigned *slow) {
+    using LY = Lay<L>;
+    using slot_t = typename LY::slot_t;
+    using out_t = typename LY::out_t;
+    constexpr int kTile = kBlock * kProbeItems;
+    constexpr int kStage = 1024;
+    constexpr int NW = kBlock / 64;
+    __shared__ out_t st_r[WRITE ? kStage : 1];
+    __shared__ out_t st_s[WRITE ? kStage : 1];
+    __shared__ unsigned st_n;
+    __shared__ unsigned long long st_base;
+    __shared__ unsigned long long wsum[NW];
+
+    const slot_t *sl = (const slot_t *)t.slots;
+    const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
+    const unsigned long long ntiles = t.meta[3];
+    for (unsigned long long j = blockIdx.x; j < ntiles; j += gridDim.x) {
+        if (threadIdx.x == 0) st_n = 0u;
+        const long long base = (long long)slow[j] * kTile + threadIdx.x;
+        unsigned long long K[kProbeItems], P[kProbeItems];
+        bool V[kProbeItems];
+#pragma unroll
+        for (int i = 0; i < kProbeItems; ++i) {
+            const long long row = base + (long long)i * kBlock;
+            V[i] = row < src.n;
+            Tuple tp = V[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
+            K[i] = tp.k;
+            P[i] = tp.p;
+        }
+        __syncthreads();   // st_n visible
+
+        unsigned long long cnt = 0;
+        auto emit = [&](unsigned long long rv, unsigned long long sv) {
+            if constexpr (!WRITE) {
+                ++cnt;
+            } else {
+                const unsigned idx = atomicAdd(&st_n, 1u);
+                if (idx < (unsigned)kStage) {
+                    st_r[idx] = (out_t)rv;
+                    st_s[idx] = (out_t)sv;
+                } else {
+                    const unsigned long long g = atomicAdd(out.counter, 1ull);
+                    if (g < (unsigned long long)out.cap) {
+                        ((out_t *)out.r)[g] = (out_t)rv;
+                        ((out_t *)out.s)[g] = (out_t)sv;
+                    }
+                }
+            }
+        };
+
+        int it = -1;
+        bool have = false;
+        unsigned long long k = 0, p = 0, hh = 0;
+        while (true) {
+            while (!have) {
+                if (++it >= kProbeItems) break;
+                if (!pick(V, it)) continue;
+                k = pick(K, it);
+                p = pick(P, it);
+                if (LY::null_key(k)) {   // wide: INT64_MIN probe key matches every side row
+                    const unsigned long long ns = t.meta[0];
+                    for (unsigned long long q = 0; q < ns; ++q) emit(t.side[q], p);
+                    continue;
+                }
+                hh = slot_of(k, t.shift);
+                have = true;
+            }
+            if (!have) break;
+            const slot_t s = sl[hh];
+            if (LY::empty(s)) {
+                have = false;
+            } else {
+                if (LY::key(s) == k) {
+                    emit(LY::pay(s), p);
+                    if (unique) have = false;
+                }
+                hh = (hh + 1) & t.mask;
+            }
+        }
+
+        if constexpr (WRITE) {
+            __syncthreads();
+            const unsigned nb = st_n;
+            const unsigned nl = nb < (unsigned)kStage ? nb : (unsigned)kStage;
+            if (threadIdx.x == 0) st_base = nl ? atomicAdd(out.counter, (unsigned long long)nl) : 0ull;
+            __syncthreads();
+            const unsigned long long gb = st_base;
+            out_t *orr = (out_t *)out.r;
+            out_t *oss = (out_t *)out.s;
+            for (unsigned q = threadIdx.x; q < nl; q += kBlock) {
+                const unsigned long long g = gb + q;
+                if (g < (unsigned long long)out.cap) {
+                    orr[g] = st_r[q];
+                    oss[g] = st_s[q];
+                }
+            }
+        } else {
+            unsigned long long c = cnt;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+            if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long tot = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) tot += wsum[w];
+                if (tot) atomicAdd(out.counter, tot);
+            }
+        }
+        __syncthreads();   // st_n / staging reused by the next tile
     }
 }
 
@@ -444,14 +561,28 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
     return hipGetLastError();
 }
 
+size_t probe_tiles(long long n) { return (size_t)(n > 0 ? (n + kBlock * kProbeItems - 1) / (kBlock * kProbeItems) : 0); }
+
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
-                        bool count_only, hipStream_t st) {
+                        bool count_only, unsigned *slow, hipStream_t st) {
     if (src.n <= 0) return hipSuccess;
     const unsigned g = grid_for(src.n, kBlock * kProbeItems);
-#define HJ_PROBE(L, F)                                                                             \
-    do {                                                                                           \
-        if (count_only) hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out); \
-        else hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out); \
+    hipError_t e = hipMemsetAsync(&t.meta[3], 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned gs = g < (unsigned)(cus * 8) ? g : (unsigned)(cus * 8);
+#define HJ_PROBE(L, F)                                                                                        \
+    do {                                                                                                      \
+        if (count_only) {                                                                                     \
+            hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow);      \
+            hipLaunchKernelGGL((k_probe_slow<L, F, false>), dim3(gs), dim3(kBlock), 0, st, t, src, out,       \
+                               (const unsigned *)slow);                                                       \
+        } else {                                                                                              \
+            hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow);       \
+            hipLaunchKernelGGL((k_probe_slow<L, F, true>), dim3(gs), dim3(kBlock), 0, st, t, src, out,        \
+                               (const unsigned *)slow);                                                       \
+        }                                                                                                     \
     } while (0)
     if (layout == kWide) {
         if (src.form == kCols64) HJ_PROBE(kWide, kCols64);

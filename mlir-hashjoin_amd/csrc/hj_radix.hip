@@ -1070,11 +1070,20 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     unsigned *work_owner = work_start + P + 1;
     const JoinVariant jv = join_variant();
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
-    const unsigned chb = (unsigned)kJoinSub * (unsigned)((jv.nt * kJoinItems) >> kFinalPbl);
-    chunk_map(s.pstart, r.pstart, P, chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    // persistent grid: as many workgroups as fit at once (LDS-limited)
+    const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
+    const unsigned pg = (unsigned)(per_cu * cu_count());
+    // S buckets per work item: at least kJoinSub sub-chunks, more when S is
+    // large against the partition count (each item rebuilds its R table), as
+    // long as ~16 items per workgroup remain for balance
+    const unsigned subb = (unsigned)((jv.nt * kJoinItems) >> kFinalPbl);
+    u64 chb = (u64)kJoinSub * subb;
+    const u64 want = (u64)s_buckets / (16ull * pg);
+    if (want > chb) chb = (want + subb - 1) / subb * subb;
+    chunk_map(s.pstart, r.pstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_buckets / chb + (u64)P + 1);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
-                       (const unsigned *)work_owner, (const u64 *)s.pstart, (const u64 *)r.pstart, P, chb,
+                       (const unsigned *)work_owner, (const u64 *)s.pstart, (const u64 *)r.pstart, P, (unsigned)chb,
                        (ItemDesc *)desc);
     JoinArgs a;
     a.r = r.rows;
@@ -1092,9 +1101,6 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.cap = cap;
     a.counter = counter;
     a.dup_flag = dup_flag;
-    // persistent grid: as many workgroups as fit at once (LDS-limited)
-    const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
-    const unsigned pg = (unsigned)(per_cu * cu_count());
     const unsigned grid = items < pg ? items : pg;
 #define HJ_JOIN(W, WR, TSL, NT) hipLaunchKernelGGL((k_join<W, WR, TSL, NT>), dim3(grid), dim3(NT), 0, st, a)
 #define HJ_JOIN_V(W, WR)                              \

@@ -87,6 +87,18 @@ class HashJoin:
     def capacity(self):
         return int(lib.hj_ctx_table_capacity(self._ctx))
 
+    @property
+    def radix_plan(self):
+        """Fan-out bits per partition pass of the current radix build ([] for global)."""
+        n = C.c_int(0)
+        bits = (C.c_int * 3)()
+        check(lib.hj_ctx_radix_plan(self._ctx, C.byref(n), bits), "hj_ctx_radix_plan")
+        return [bits[i] for i in range(n.value)]
+
+    @property
+    def radix_passes(self):
+        return len(self.radix_plan)
+
     def has_duplicates(self):
         r = lib.hj_ctx_build_has_duplicates(self._ctx)
         if r < 0:
