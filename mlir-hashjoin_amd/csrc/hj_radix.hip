@@ -951,7 +951,8 @@ RadixPlan radix_plan(long long n_build, int force_bits) {
 
 // Pass i writes the final set when (passes - 1 - i) is even, else the ping
 // set.  It allocates at most n / PB full buckets plus one open bucket per
-// (workgroup segment run, bin): runs <= G + nseg_in.
+// (workgroup segment run, bin): runs <= G + nseg_in; and a bucket is only
+// allocated to take rows.
 RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
     RadixNeed need{1, 1};
     const u64 rows = n > 0 ? (u64)n : 1;
@@ -959,7 +960,9 @@ RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
     for (int i = 0; i < pl.passes; ++i) {
         const bool to_final = ((pl.passes - 1 - i) % 2) == 0;
         const u64 F = 1ull << pl.bits[i];
-        const u64 b = (rows >> pl.pbl[i]) + ((u64)pass_grid(rows) + nseg + 1) * F + 1;
+        // every bucket holds >= 1 row, so never more than `rows` buckets
+        const u64 open = ((u64)pass_grid(rows) + nseg + 1) * F;
+        const u64 b = (rows >> pl.pbl[i]) + (open < rows ? open : rows) + 1;
         if (to_final == final_set) {
             if (b > need.buckets) need.buckets = b;
             if ((b << pl.pbl[i]) > need.rows) need.rows = b << pl.pbl[i];

@@ -121,6 +121,39 @@ def test_radix_count_and_capacity(hj, oracle):
     assert oracle.same_multiset(*o, *exp)
 
 
+@pytest.mark.parametrize("bits", [12, 17])
+def test_radix_many_workgroups_vs_oracle(hj, oracle, bits):
+    """2^20 rows: every workgroup owns many tiles and (pass 2) several
+    segments, so open buckets are closed on segment switches and at the end;
+    partitions are lists of full and partial buckets from several writers."""
+    n = 1 << 20
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(bits + 100, n, n + 12345, 0.8)
+    o = run(hj, rk, rp, sk, sp, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=n // 16))
+
+
+def test_radix_unaligned_columns_and_tuples(hj, oracle):
+    """Pass 1 reads two columns 16 B at a time when both are 16-B aligned;
+    views offset by one element take the 8-B path.  Packed tuples too."""
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(77, 50001, 70003, 0.6)
+    exp = oracle.chained_join_i64(rk[1:], rp[1:], sk[1:], sp[1:], H=500)
+    R = [dev(rk), dev(rp)]; S = [dev(sk), dev(sp)]
+    hj.set_strategy("radix", radix_bits=11)
+    try:
+        o_r, o_s = hj.join(R[0][1:], R[1][1:], S[0][1:], S[1][1:])
+        assert R[0][1:].data_ptr() % 16 == 8
+        assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp)
+        tr = torch.stack([R[0][1:], R[1][1:]], 1).contiguous()
+        ts = torch.stack([S[0][1:], S[1][1:]], 1).contiguous()
+        hj.build_tuples(tr)
+        assert hj.strategy_used == "radix"
+        out_r = torch.empty(ts.shape[0], dtype=torch.int64, device="cuda"); out_s = torch.empty_like(out_r)
+        m = int(hj.probe_tuples(ts, out_r, out_s).item())
+        assert oracle.same_multiset(out_r[:m].cpu().numpy(), out_s[:m].cpu().numpy(), *exp)
+    finally:
+        hj.set_strategy("auto")
+
+
 def test_strategies_agree_full_size(hj):
     """C1 at 2^24: global and radix strategies give the same pair set."""
     n = 1 << 24
