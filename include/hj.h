@@ -157,6 +157,20 @@ int hj_dev_gen_uniform_i64(uint64_t seed, uint64_t stream_id, int64_t lo, int64_
 int hj_dev_gen_uniform_i32(uint64_t seed, uint64_t stream_id, int32_t lo, int32_t hi,
                            int64_t i0, int64_t n, int32_t *key, void *stream);
 
+/* nested-loop.mlir result rows (:29-192, @main :195-289).  Row-major int32
+ * tables with the key in column 0 and row strides ld1 / ld2 (elements).
+ * Roles as %table_1_or_2_as_inner (:247): the larger table is the outer X
+ * (ties: t1), the smaller the inner Y; every pair X[i][0] == Y[j][0] yields
+ * the row [X[i][0 .. cx), Y[j][1 .. cy)] (cx + cy - 1 columns).  Executed as
+ * a hash join (build Y, probe X) plus a row gather.  d_count = M; rows past
+ * out_cap are dropped.  Rows are in no particular order (as the reference's
+ * atomic block offsets). */
+int hj_dev_count_rows_i32(hj_ctx *ctx, const int32_t *t1, int64_t r1, int64_t c1, int64_t ld1, const int32_t *t2,
+                          int64_t r2, int64_t c2, int64_t ld2, uint64_t *d_count, void *stream);
+int hj_dev_join_rows_i32(hj_ctx *ctx, const int32_t *t1, int64_t r1, int64_t c1, int64_t ld1, const int32_t *t2,
+                         int64_t r2, int64_t c2, int64_t ld2, int32_t *out, int64_t ldo, int64_t out_cap,
+                         uint64_t *d_count, void *stream);
+
 /* ------------------------------------------------------- host memref ABI
  * Two-phase, reference-shaped (mirrors @countRows -> alloc -> @probeRelation,
  * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion.  Both calls
@@ -181,6 +195,19 @@ int32_t hj_probe_i64(int64_t *rk_alloc, int64_t *rk_align, int64_t rk_off, int64
                      int64_t *or_alloc, int64_t *or_align, int64_t or_off, int64_t or_size, int64_t or_stride,
                      int64_t *os_alloc, int64_t *os_align, int64_t os_off, int64_t os_size, int64_t os_stride);
 
+/* nested-loop.mlir rows over host 2-D memrefs (7 scalars each: allocated,
+ * aligned, offset, sizes[2], strides[2]).  hj_join_rows_i32 writes the M rows
+ * into the result memref (>= M rows, c1 + c2 - 1 columns) and returns M, or
+ * < 0 (HJ_ERR_CAPACITY when the result has fewer than M rows). */
+int64_t hj_count_rows_i32(int32_t *t1_alloc, int32_t *t1_align, int64_t t1_off, int64_t t1_rows, int64_t t1_cols,
+                          int64_t t1_s0, int64_t t1_s1, int32_t *t2_alloc, int32_t *t2_align, int64_t t2_off,
+                          int64_t t2_rows, int64_t t2_cols, int64_t t2_s0, int64_t t2_s1);
+int64_t hj_join_rows_i32(int32_t *t1_alloc, int32_t *t1_align, int64_t t1_off, int64_t t1_rows, int64_t t1_cols,
+                         int64_t t1_s0, int64_t t1_s1, int32_t *t2_alloc, int32_t *t2_align, int64_t t2_off,
+                         int64_t t2_rows, int64_t t2_cols, int64_t t2_s0, int64_t t2_s1, int32_t *o_alloc,
+                         int32_t *o_align, int64_t o_off, int64_t o_rows, int64_t o_cols, int64_t o_s0,
+                         int64_t o_s1);
+
 /* ------------------------------------------------------ MLIR C-interface
  * Descriptor structs of memref<?xT> / memref<?x2xT> (MLIR's StridedMemRefType
  * layout: allocated, aligned, offset, sizes[rank], strides[rank]). */
@@ -197,6 +224,9 @@ void _mlir_ciface_hj_join_i64(hj_memref2_i64 *result, hj_memref1_i64 *r, hj_memr
 /* key/payload column pairs -> memref<?x2xi64> (R.pay, S.pay). */
 void _mlir_ciface_hj_join_kp_i64(hj_memref2_i64 *result, hj_memref1_i64 *rkey, hj_memref1_i64 *rpay,
                                  hj_memref1_i64 *skey, hj_memref1_i64 *spay);
+/* memref<?x?xi32> tables -> memref<?x?xi32> rows of nested-loop.mlir
+ * (exactly M rows, malloc'ed). */
+void _mlir_ciface_hj_join_rows_i32(hj_memref2_i32 *result, hj_memref2_i32 *t1, hj_memref2_i32 *t2);
 /* Release a result buffer of the ciface joins (== free(allocated)). */
 void hj_free_result(void *allocated);
 

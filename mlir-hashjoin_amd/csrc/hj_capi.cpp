@@ -113,6 +113,7 @@ struct hj_ctx {
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
     Buf nb, pcur, tile_start, tile_owner, work_start, work_desc, scan_sums;
     Buf slow;   // global-table probe: tiles for the general path
+    Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -395,6 +396,51 @@ hj_ctx *default_ctx() {
     return c;
 }
 
+// nested-loop.mlir (:29-192, @main :195-289) as a hash join plus a row
+// gather.  Roles as %table_1_or_2_as_inner (:247): the larger table is the
+// outer X (ties: t1), the smaller the inner Y; every pair X[i][0] == Y[j][0]
+// yields the row [X[i][0 .. cx), Y[j][1 .. cy)].  Y is the build side (i32
+// keys, payload = row id), X probes; pair row ids are staged in ctx buffers
+// and k_gather_rows_i32 writes the rows (<= cap of them; *d_count = M).
+struct RowTables {
+    const int32_t *t1;
+    int64_t r1, c1, ld1;
+    const int32_t *t2;
+    int64_t r2, c2, ld2;
+};
+
+int do_join_rows(hj_ctx *c, const RowTables &a, int32_t *out, int64_t ldo, int64_t cap, uint64_t *d_count,
+                 bool count_only, hipStream_t st) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (!d_count) HJ_FAIL(HJ_ERR_ARG, "null count pointer");
+    if (a.r1 < 0 || a.r2 < 0 || a.c1 < 1 || a.c2 < 1 || a.ld1 < a.c1 || a.ld2 < a.c2)
+        HJ_FAIL(HJ_ERR_ARG, "bad table shape");
+    if ((a.r1 > 0 && !a.t1) || (a.r2 > 0 && !a.t2)) HJ_FAIL(HJ_ERR_ARG, "null table");
+    if (a.r1 > 0x7fffffffll || a.r2 > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids: tables must have < 2^31 rows");
+    const bool t2_outer = a.r1 < a.r2;   // nested-loop.mlir:247
+    const int32_t *x = t2_outer ? a.t2 : a.t1, *y = t2_outer ? a.t1 : a.t2;
+    const int64_t rx = t2_outer ? a.r2 : a.r1, cx = t2_outer ? a.c2 : a.c1, ldx = t2_outer ? a.ld2 : a.ld1;
+    const int64_t ry = t2_outer ? a.r1 : a.r2, cy = t2_outer ? a.c1 : a.c2, ldy = t2_outer ? a.ld1 : a.ld2;
+    const int64_t oc = cx + cy - 1;
+    if (!count_only && (cap < 0 || (cap > 0 && (!out || ldo < oc)))) HJ_FAIL(HJ_ERR_ARG, "bad row output");
+    HJ_TRY(set_device(c));
+    HJ_TRY(ensure_buf(c->rows_kx, (size_t)(rx > 0 ? rx : 1) * 4));
+    HJ_TRY(ensure_buf(c->rows_ky, (size_t)(ry > 0 ? ry : 1) * 4));
+    int32_t *kx = (int32_t *)c->rows_kx.p, *ky = (int32_t *)c->rows_ky.p;
+    HJ_HIP(hj::launch_key_col_i32(x, rx, ldx, kx, st));
+    HJ_HIP(hj::launch_key_col_i32(y, ry, ldy, ky, st));
+    HJ_TRY(do_build(c, kNarrow, src_col32(ky, ry, 0), st));
+    if (count_only) return do_probe(c, kNarrow, src_col32(kx, rx, 0), nullptr, nullptr, 0, d_count, true, st);
+    HJ_TRY(ensure_buf(c->rows_px, (size_t)(cap > 0 ? cap : 1) * 4));
+    HJ_TRY(ensure_buf(c->rows_py, (size_t)(cap > 0 ? cap : 1) * 4));
+    int32_t *px = (int32_t *)c->rows_px.p, *py = (int32_t *)c->rows_py.p;
+    // R payload = Y row, S payload = X row
+    HJ_TRY(do_probe(c, kNarrow, src_col32(kx, rx, 0), py, px, cap, d_count, false, st));
+    HJ_HIP(hj::launch_gather_rows_i32(x, ldx, (int)cx, y, ldy, (int)cy, px, py, (const unsigned long long *)d_count,
+                                      cap, out, ldo, st));
+    return HJ_OK;
+}
+
 int dbuf(hj_ctx *c, int i, size_t bytes, void **p) {
     if (bytes == 0) bytes = 16;
     if (c->dbuf_bytes[i] < bytes) {
@@ -575,6 +621,59 @@ int fill_result(D *res, const void *d_r, const void *d_s, int64_t m, hipStream_t
 
 }  // namespace
 
+namespace {
+
+// Upload a strided 2-D host memref (aligned + offset, sizes, strides) as a
+// contiguous row-major rows x cols block.
+int upload2(void *dst, const int32_t *aligned, int64_t off, int64_t rows, int64_t cols, int64_t s0, int64_t s1,
+            hipStream_t st) {
+    if (rows <= 0 || cols <= 0) return HJ_OK;
+    if (!aligned) HJ_FAIL(HJ_ERR_ARG, "null memref");
+    const int32_t *base = aligned + off;
+    if (s1 == 1 && s0 == cols) {
+        HJ_HIP(hipMemcpyAsync(dst, base, sizeof(int32_t) * (size_t)(rows * cols), hipMemcpyHostToDevice, st));
+    } else {
+        std::vector<int32_t> tmp((size_t)(rows * cols));
+        for (int64_t i = 0; i < rows; ++i)
+            for (int64_t j = 0; j < cols; ++j) tmp[(size_t)(i * cols + j)] = base[i * s0 + j * s1];
+        HJ_HIP(hipMemcpyAsync(dst, tmp.data(), sizeof(int32_t) * tmp.size(), hipMemcpyHostToDevice, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        return HJ_OK;
+    }
+    HJ_HIP(hipStreamSynchronize(st));
+    return HJ_OK;
+}
+
+// Host-memref row join: tables copied in, rows materialised on the device
+// into staging buffer dbuf[4] (M x oc, contiguous); *m = M, *oc_out = columns.
+int host_join_rows(hj_ctx *c, const int32_t *a1, int64_t o1, int64_t r1, int64_t c1, int64_t s10, int64_t s11,
+                   const int32_t *a2, int64_t o2, int64_t r2, int64_t c2, int64_t s20, int64_t s21, bool count_only,
+                   int64_t *m, int64_t *oc_out, void **d_out) {
+    if (r1 < 0 || r2 < 0 || c1 < 1 || c2 < 1) HJ_FAIL(HJ_ERR_ARG, "bad memref shape");
+    HJ_TRY(set_device(c));
+    HJ_TRY(host_stream(c));
+    hipStream_t st = c->host_stream;
+    void *d1, *d2;
+    HJ_TRY(dbuf(c, 0, sizeof(int32_t) * (size_t)(r1 * c1), &d1));
+    HJ_TRY(dbuf(c, 1, sizeof(int32_t) * (size_t)(r2 * c2), &d2));
+    HJ_TRY(upload2(d1, a1, o1, r1, c1, s10, s11, st));
+    HJ_TRY(upload2(d2, a2, o2, r2, c2, s20, s21, st));
+    const RowTables t{(const int32_t *)d1, r1, c1, c1, (const int32_t *)d2, r2, c2, c2};
+    *oc_out = c1 + c2 - 1;
+    uint64_t cnt = 0;
+    HJ_TRY(do_join_rows(c, t, nullptr, 0, 0, (uint64_t *)c->dcount, true, st));
+    HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    *m = (int64_t)cnt;
+    if (count_only) return HJ_OK;
+    HJ_TRY(dbuf(c, 4, sizeof(int32_t) * (size_t)(*m > 0 ? *m * *oc_out : 1), d_out));
+    HJ_TRY(do_join_rows(c, t, (int32_t *)*d_out, *oc_out, *m, (uint64_t *)c->dcount, false, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    return HJ_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int hj_abi_version(void) { return HJ_ABI_VERSION; }
@@ -613,7 +712,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
     for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums,
-                   &c->slow})
+                   &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py})
         free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -957,6 +1056,90 @@ void _mlir_ciface_hj_join_kp_i64(hj_memref2_i64 *res, hj_memref1_i64 *rk, hj_mem
                       sp->strides[0], sk->sizes[0], false, &m, &d_or, &d_os) != HJ_OK)
         return;
     fill_result<int64_t>(res, d_or, d_os, m, c->host_stream);
+}
+
+// ------------------------------------------------- nested-loop.mlir rows
+int hj_dev_count_rows_i32(hj_ctx *c, const int32_t *t1, int64_t r1, int64_t c1, int64_t ld1, const int32_t *t2,
+                          int64_t r2, int64_t c2, int64_t ld2, uint64_t *d_count, void *stream) {
+    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), (hipStream_t)stream));
+    return do_join_rows(c, RowTables{t1, r1, c1, ld1, t2, r2, c2, ld2}, nullptr, 0, 0, d_count, true,
+                        (hipStream_t)stream);
+}
+
+int hj_dev_join_rows_i32(hj_ctx *c, const int32_t *t1, int64_t r1, int64_t c1, int64_t ld1, const int32_t *t2,
+                         int64_t r2, int64_t c2, int64_t ld2, int32_t *out, int64_t ldo, int64_t out_cap,
+                         uint64_t *d_count, void *stream) {
+    return do_join_rows(c, RowTables{t1, r1, c1, ld1, t2, r2, c2, ld2}, out, ldo, out_cap, d_count, false,
+                        (hipStream_t)stream);
+}
+
+int64_t hj_count_rows_i32(int32_t *, int32_t *a1, int64_t o1, int64_t r1, int64_t c1, int64_t s10, int64_t s11,
+                          int32_t *, int32_t *a2, int64_t o2, int64_t r2, int64_t c2, int64_t s20, int64_t s21) {
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0, oc = 0;
+    void *d = nullptr;
+    const int rc = host_join_rows(c, a1, o1, r1, c1, s10, s11, a2, o2, r2, c2, s20, s21, true, &m, &oc, &d);
+    return rc == HJ_OK ? m : rc;
+}
+
+int64_t hj_join_rows_i32(int32_t *, int32_t *a1, int64_t o1, int64_t r1, int64_t c1, int64_t s10, int64_t s11,
+                         int32_t *, int32_t *a2, int64_t o2, int64_t r2, int64_t c2, int64_t s20, int64_t s21,
+                         int32_t *, int32_t *ao, int64_t oo, int64_t ro, int64_t co, int64_t so0, int64_t so1) {
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    int64_t m = 0, oc = 0;
+    void *d = nullptr;
+    HJ_TRY(host_join_rows(c, a1, o1, r1, c1, s10, s11, a2, o2, r2, c2, s20, s21, false, &m, &oc, &d));
+    if (co != oc) HJ_FAIL(HJ_ERR_ARG, "result memref must have c1 + c2 - 1 columns");
+    if (ro < m) HJ_FAIL(HJ_ERR_CAPACITY, "result memref has fewer rows than the join");
+    if (m > 0) {
+        if (!ao) HJ_FAIL(HJ_ERR_ARG, "null result memref");
+        std::vector<int32_t> tmp((size_t)(m * oc));
+        HJ_HIP(hipMemcpyAsync(tmp.data(), d, sizeof(int32_t) * tmp.size(), hipMemcpyDeviceToHost, c->host_stream));
+        HJ_HIP(hipStreamSynchronize(c->host_stream));
+        int32_t *base = ao + oo;
+        for (int64_t i = 0; i < m; ++i)
+            for (int64_t j = 0; j < oc; ++j) base[i * so0 + j * so1] = tmp[(size_t)(i * oc + j)];
+    }
+    return m;
+}
+
+void _mlir_ciface_hj_join_rows_i32(hj_memref2_i32 *res, hj_memref2_i32 *t1, hj_memref2_i32 *t2) {
+    if (!res) return;
+    std::memset(res, 0, sizeof(*res));
+    if (!t1 || !t2) {
+        fail(HJ_ERR_ARG, __FILE__, __LINE__, "null memref descriptor");
+        return;
+    }
+    hj_ctx *c = default_ctx();
+    if (!c) return;
+    int64_t m = 0, oc = 0;
+    void *d = nullptr;
+    if (host_join_rows(c, t1->aligned, t1->offset, t1->sizes[0], t1->sizes[1], t1->strides[0], t1->strides[1],
+                       t2->aligned, t2->offset, t2->sizes[0], t2->sizes[1], t2->strides[0], t2->strides[1], false,
+                       &m, &oc, &d) != HJ_OK)
+        return;
+    int32_t *h = (int32_t *)std::malloc(sizeof(int32_t) * (size_t)(m > 0 ? m * oc : 1));
+    if (!h) {
+        fail(HJ_ERR_NOMEM, __FILE__, __LINE__, "malloc result");
+        return;
+    }
+    if (m > 0) {
+        if (hipMemcpyAsync(h, d, sizeof(int32_t) * (size_t)(m * oc), hipMemcpyDeviceToHost, c->host_stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(c->host_stream) != hipSuccess) {
+            std::free(h);
+            fail(HJ_ERR_HIP, __FILE__, __LINE__, "copy result");
+            return;
+        }
+    }
+    res->allocated = res->aligned = h;
+    res->offset = 0;
+    res->sizes[0] = m;
+    res->sizes[1] = oc;
+    res->strides[0] = oc;
+    res->strides[1] = 1;
 }
 
 void hj_free_result(void *allocated) { std::free(allocated); }

@@ -127,6 +127,12 @@ hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
                             hipStream_t st);
 
+// nested-loop.mlir result rows (hj_kernels.hip)
+hipError_t launch_key_col_i32(const int *t, long long rows, long long ld, int *out, hipStream_t st);
+hipError_t launch_gather_rows_i32(const int *x, long long ldx, int cx, const int *y, long long ldy, int cy,
+                                  const int *px, const int *py, const unsigned long long *count, long long cap,
+                                  int *out, long long ldo, hipStream_t st);
+
 hipError_t launch_gen_pkfk(unsigned long long seed, long long NR, unsigned long long hit_thr,
                            long long r0, long long nr, long long *rkey, long long *rpay,
                            long long s0, long long ns, long long *skey, long long *spay,

@@ -531,6 +531,31 @@ __global__ __launch_bounds__(kBlock) void k_gen_zipf(unsigned long long seed, Zi
     spay[i] = (long long)g;
 }
 
+// ------------------------------------------------------------------ rows
+// nested-loop.mlir's result rows (:160-188) materialised from join pairs.
+// Key column (column 0) of a row-major int32 table with row stride ld.
+__global__ __launch_bounds__(kBlock) void k_key_col_i32(const int *t, long long rows, long long ld, int *out) {
+    const long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (i < rows) out[i] = t[i * ld];
+}
+
+// out[m] = [X[px[m]][0 .. cx), Y[py[m]][1 .. cy)] for m < min(*count, cap):
+// one lane per output element, so the stores are coalesced and the row
+// gathers are the only scattered accesses.
+__global__ __launch_bounds__(kBlock) void k_gather_rows_i32(const int *x, long long ldx, int cx, const int *y,
+                                                            long long ldy, int cy, const int *px, const int *py,
+                                                            const unsigned long long *count, long long cap,
+                                                            int *out, long long ldo) {
+    const int oc = cx + cy - 1;
+    const unsigned long long m_all = *count;
+    const long long m = (long long)(m_all < (unsigned long long)cap ? m_all : (unsigned long long)cap);
+    for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < m * oc; e += (long long)gridDim.x * kBlock) {
+        const long long r = e / oc;
+        const int c = (int)(e - r * oc);
+        out[r * ldo + c] = c < cx ? x[(long long)px[r] * ldx + c] : y[(long long)py[r] * ldy + (c - cx + 1)];
+    }
+}
+
 inline unsigned grid_for(long long n, int per_block) {
     return (unsigned)((n + per_block - 1) / per_block);
 }
@@ -647,6 +672,24 @@ hipError_t launch_gen_uniform_i32(unsigned long long seed, unsigned long long si
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_gen_uniform_i32, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, seed, sid, lo, hi, i0, n,
                        key);
+    return hipGetLastError();
+}
+
+hipError_t launch_key_col_i32(const int *t, long long rows, long long ld, int *out, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_key_col_i32, dim3(grid_for(rows, kBlock)), dim3(kBlock), 0, st, t, rows, ld, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows_i32(const int *x, long long ldx, int cx, const int *y, long long ldy, int cy,
+                                  const int *px, const int *py, const unsigned long long *count, long long cap,
+                                  int *out, long long ldo, hipStream_t st) {
+    if (cap <= 0) return hipSuccess;
+    const long long elems = cap * (long long)(cx + cy - 1);
+    unsigned g = grid_for(elems, kBlock * 4);
+    if (g > 65536u) g = 65536u;   // grid-stride beyond
+    hipLaunchKernelGGL(k_gather_rows_i32, dim3(g), dim3(kBlock), 0, st, x, ldx, cx, y, ldy, cy, px, py, count, cap,
+                       out, ldo);
     return hipGetLastError();
 }
 

@@ -81,6 +81,12 @@ def _load():
         "hj_probe_i32": (C.c_int32, [_vp, _vp, _i64, _i64, _i64] * 4),
         "hj_count_i64": (_i64, [_vp, _vp, _i64, _i64, _i64] * 4),
         "hj_probe_i64": (C.c_int32, [_vp, _vp, _i64, _i64, _i64] * 6),
+        "hj_dev_count_rows_i32": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _vp]),
+        "hj_dev_join_rows_i32": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp,
+                                        _vp]),
+        "hj_count_rows_i32": (_i64, [_vp, _vp, _i64, _i64, _i64, _i64, _i64] * 2),
+        "hj_join_rows_i32": (_i64, [_vp, _vp, _i64, _i64, _i64, _i64, _i64] * 3),
+        "_mlir_ciface_hj_join_rows_i32": (None, [_vp, _vp, _vp]),
         "_mlir_ciface_hj_join_i32": (None, [_vp, _vp, _vp]),
         "_mlir_ciface_hj_join_i64": (None, [_vp, _vp, _vp]),
         "_mlir_ciface_hj_join_kp_i64": (None, [_vp, _vp, _vp, _vp, _vp]),

@@ -197,6 +197,28 @@ class HashJoin:
         return out, counts
 
     # -------------------------------------------------------------- whole join
+    def join_rows(self, t1, t2, stream=None):
+        """nested-loop.mlir (:29-192) on device: t1, t2 are 2-D int32 tensors
+        (row-major, key in column 0); returns the (M, c1 + c2 - 1) int32 rows
+        [X row, Y cols 1..] of every key match, X the larger table (ties: t1).
+        Count first, then materialise exactly M rows.  Row strides may exceed
+        the column count (column slices of wider tables)."""
+        for t in (t1, t2):
+            if not t.is_cuda:
+                raise ValueError("hash join inputs must be device tensors")
+            if t.dtype != torch.int32 or t.dim() != 2 or (t.numel() and t.stride(1) != 1):
+                raise ValueError("tables must be 2-D int32 tensors with unit column stride")
+        ld = [t.stride(0) if t.numel() else t.shape[1] for t in (t1, t2)]
+        st = _stream(self.device, stream)
+        args = (_ptr(t1), t1.shape[0], t1.shape[1], ld[0], _ptr(t2), t2.shape[0], t2.shape[1], ld[1])
+        check(lib.hj_dev_count_rows_i32(self._ctx, *args, _ptr(self._count), st), "hj_dev_count_rows_i32")
+        m = int(self._count.item())
+        oc = t1.shape[1] + t2.shape[1] - 1
+        out = torch.empty((max(m, 1), oc), dtype=torch.int32, device=t1.device)
+        check(lib.hj_dev_join_rows_i32(self._ctx, *args, _ptr(out), oc, m, _ptr(self._count), st),
+              "hj_dev_join_rows_i32")
+        return out[:m]
+
     def join(self, rkey, rpay, skey, spay=None, capacity=None, stream=None):
         """The @main join (join_v2.mlir:646-696) on device tensors: build, then
         probe into an output sized optimistically (|S| rows, or `capacity`),

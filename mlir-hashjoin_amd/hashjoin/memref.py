@@ -58,6 +58,50 @@ def join_i32_two_phase(r, s):
     return out_r, out_s
 
 
+def expand2(a: np.ndarray, base: np.ndarray | None = None):
+    """7-scalar expansion of a 2-D memref<?x?xT> view (allocated, aligned,
+    offset, sizes[2], strides[2], all in elements)."""
+    base = a if base is None else base
+    item = a.itemsize
+    if a.ndim != 2 or a.strides[0] % item or a.strides[1] % item:
+        raise ValueError("2-D element-strided view required")
+    ptr = base.ctypes.data
+    off = (a.ctypes.data - ptr) // item
+    return [C.c_void_p(ptr), C.c_void_p(ptr), off, a.shape[0], a.shape[1], a.strides[0] // item,
+            a.strides[1] // item]
+
+
+def count_rows_i32(t1, t2):
+    """nested-loop.mlir result row count through hj_count_rows_i32."""
+    return int(lib.hj_count_rows_i32(*expand2(t1), *expand2(t2)))
+
+
+def join_rows_i32(t1, t2, out):
+    """nested-loop.mlir rows into the 2-D result memref `out`; returns M."""
+    return int(lib.hj_join_rows_i32(*expand2(t1), *expand2(t2), *expand2(out)))
+
+
+def ciface_join_rows_i32(t1, t2):
+    """_mlir_ciface_hj_join_rows_i32: memref<?x?xi32> x2 -> memref<?x?xi32> rows."""
+    t1 = np.ascontiguousarray(t1, np.int32); t2 = np.ascontiguousarray(t2, np.int32)
+    res = MemRef2I32()
+    ds = []
+    for t in (t1, t2):
+        d = MemRef2I32()
+        p = t.ctypes.data_as(C.POINTER(C.c_int32))
+        d.allocated = p; d.aligned = p; d.offset = 0
+        d.sizes[0], d.sizes[1] = t.shape
+        d.strides[0], d.strides[1] = t.shape[1], 1
+        ds.append(d)
+    lib._mlir_ciface_hj_join_rows_i32(C.byref(res), C.byref(ds[0]), C.byref(ds[1]))
+    if not res.allocated:
+        raise RuntimeError("ciface join failed: " + lib.hj_last_error().decode())
+    m, oc = res.sizes[0], res.sizes[1]
+    out = np.ctypeslib.as_array(res.aligned, shape=(max(m * oc, 1),))[: m * oc].reshape(m, oc).copy()
+    lib.hj_free_result(C.cast(res.allocated, C.c_void_p))
+    return out
+
+
 def _desc1(a, cls):
     d = cls()
     ct = _CT[a.dtype]
