@@ -269,7 +269,10 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, u
 // [w*T/G, (w+1)*T/G); its open bucket per bin lives in LDS (cur, fill) and
 // is closed (bfill written) when the workgroup moves to another segment or
 // finishes, so at most (G + nseg) * F buckets are ever partly filled.
-template <bool WIDE, int FORM>
+// ABL (diagnostics only, micro/pass_micro.hip; the product uses 0): 1 no row
+// stores, 2 synthetic rows instead of loads, 4 rows stored back in tile order
+// (contiguous) instead of to their buckets, 8 runs start on 128-B lines.
+template <bool WIDE, int FORM, int ABL = 0>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -277,6 +280,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ T stage[kTile];
     __shared__ unsigned short sb[kTile];
     __shared__ unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan], nbase[kMaxFan];
+    __shared__ unsigned s_nb;   // first fresh bucket of the current tile
     const unsigned F = 1u << a.fbits;
     const unsigned PB = 1u << a.out_pbl;
     const unsigned T_ = pass_tiles<FORM>(a);
@@ -288,6 +292,11 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         cur[b] = kNoBucket;
         fill[b] = PB;
     }
+    // ABL 8 (diagnostic): every run starts on a 128-B line (wastes space)
+    auto afill = [&](unsigned f) -> unsigned {
+        if constexpr ((ABL & 8) != 0) return f >= PB ? f : ((f + 7u) & ~7u) > PB ? PB : ((f + 7u) & ~7u);
+        return f;
+    };
     int seg_cur = -1;
     // close this workgroup's open buckets (their fill is final)
     auto close_all = [&]() {
@@ -331,6 +340,12 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         } else {
 #pragma unroll
             for (int i = 0; i < IT; ++i) {
+                if constexpr ((ABL & 2) != 0) {
+                    const u64 v = (u64)t * kTile + (u64)i * kPassThreads + threadIdx.x;
+                    row[i] = R::make(fmix64(v), v);
+                    br[i] = 0u;
+                    continue;
+                }
                 if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
                     row[i] = R::zero();
                     br[i] = 0xFFFFFFFFu;
@@ -347,49 +362,44 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         if (threadIdx.x < 64) {
-            // wave 0: exclusive scan of the bin counts, 8 bins per lane
+            // wave 0: exclusive scans of the bin counts (-> start) and of the
+            // fresh buckets each bin needs (-> nbase, relative); ONE global
+            // atomic reserves the tile's buckets (a counter hit once per bin
+            // allocation serialised ~1M atomics per 2^28-row pass)
             const int lane = threadIdx.x;
-            unsigned c[8], s = 0;
+            unsigned c[8], k[8], s = 0, sk = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const unsigned b = lane * 8 + j;
                 c[j] = b < F ? cnt[b] : 0u;
+                k[j] = c[j] ? (afill(fill[b]) + c[j] - 1) >> a.out_pbl : 0u;
                 s += c[j];
+                sk += k[j];
             }
-            unsigned x = s;
+            unsigned x = s, xk = sk;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
-                const unsigned y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
+                const unsigned y = __shfl_up(x, o, 64), yk = __shfl_up(xk, o, 64);
+                if (lane >= o) {
+                    x += y;
+                    xk += yk;
+                }
             }
-            unsigned run = x - s;
+            unsigned run = x - s, runk = xk - sk;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const unsigned b = lane * 8 + j;
-                if (b < F) start[b] = run;
-                run += c[j];
-            }
-        } else if (threadIdx.x >= kPassThreads - kMaxFan) {
-            // the last 512 threads: fresh buckets for bins whose run overflows
-            // the open one (k of them, one atomic per bin)
-            const unsigned b = threadIdx.x - (kPassThreads - kMaxFan);
-            const unsigned c = b < F ? cnt[b] : 0u;
-            if (c) {
-                const unsigned f = fill[b];
-                const unsigned k = (f + c - 1) >> a.out_pbl;
-                if (k) {
-                    const unsigned nb = atomicAdd(a.nb, k);
-                    const bool fits = (u64)nb + k <= a.max_buckets;
-                    nbase[b] = fits ? nb : kNoBucket;
-                    if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
-                    if (fits) {
-                        const unsigned pid = ((unsigned)tl.seg << a.fbits) | b;
-                        for (unsigned i = 0; i < k; ++i) {
-                            a.bbin[nb + i] = pid;
-                            if (i + 1 < k) a.bfill[nb + i] = PB;
-                        }
-                    }
+                if (b < F) {
+                    start[b] = run;
+                    nbase[b] = runk;
                 }
+                run += c[j];
+                runk += k[j];
+            }
+            if (lane == 63) {
+                unsigned nb = xk ? atomicAdd(a.nb, xk) : 0u;
+                if ((u64)nb + xk > a.max_buckets) nb = kNoBucket;   // cannot happen within radix_need
+                s_nb = nb;
             }
         }
         __syncthreads();
@@ -408,9 +418,14 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
             if (j >= tn) continue;
             const unsigned b = sb[j];
-            const unsigned p = fill[b] + (j - start[b]);
+            const unsigned p = afill(fill[b]) + (j - start[b]);
             const unsigned k = p >> a.out_pbl;
-            const unsigned bk = k == 0 ? cur[b] : (nbase[b] == kNoBucket ? kNoBucket : nbase[b] + k - 1);
+            const unsigned bk = k == 0 ? cur[b] : (s_nb == kNoBucket ? kNoBucket : s_nb + nbase[b] + k - 1);
+            if constexpr ((ABL & 1) != 0) continue;
+            if constexpr ((ABL & 4) != 0) {
+                out[(u64)t * kTile + j] = stage[j];
+                continue;
+            }
             if (bk < a.max_buckets) out[((u64)bk << a.out_pbl) + (p & (PB - 1))] = stage[j];
         }
         __syncthreads();
@@ -418,10 +433,22 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const unsigned c = cnt[b];
             cnt[b] = 0u;
             if (!c) continue;
-            const unsigned f = fill[b];
+            const unsigned f = afill(fill[b]);
             const unsigned k = (f + c - 1) >> a.out_pbl;
             if (k) {
-                cur[b] = nbase[b] == kNoBucket ? kNoBucket : nbase[b] + k - 1;
+                // the replaced open bucket is full; record the fresh ones
+                if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
+                if (s_nb != kNoBucket) {
+                    const unsigned nb = s_nb + nbase[b];
+                    const unsigned pid = ((unsigned)tl.seg << a.fbits) | b;
+                    for (unsigned i = 0; i < k; ++i) {
+                        a.bbin[nb + i] = pid;
+                        if (i + 1 < k) a.bfill[nb + i] = PB;
+                    }
+                    cur[b] = nb + k - 1;
+                } else {
+                    cur[b] = kNoBucket;
+                }
                 fill[b] = f + c - (k << a.out_pbl);
             } else {
                 fill[b] = f + c;

@@ -1,0 +1,82 @@
+// pass_micro.hip -- ablation of the partition pass kernel (k_pass) on 2^28
+// packed 16-B rows, first pass (512 bins) and a 256-bin pass.
+// ABL bits: 1 no row stores, 2 synthetic rows instead of loads, 4 rows stored
+// contiguously (tile order) instead of to their buckets.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../csrc -I../../include -o pass_micro pass_micro.hip
+#include "../csrc/hj_radix.hip"
+
+#include <cstdio>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+using namespace hj;
+typedef unsigned long long u64;
+
+__global__ void k_fill(ulonglong2 *r, u64 n) {
+    const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) r[i] = make_ulonglong2(fmix64(i * 7 + 1), i);
+}
+
+int main() {
+    const u64 n = 1ull << 28;
+    ulonglong2 *in, *out;
+    unsigned *bbin, *bfill, *nb;
+    const u64 maxb = n / 256 + (1u << 20);
+    CK(hipMalloc(&in, n * 16));
+    CK(hipMalloc(&out, maxb * 512 * 16));
+    CK(hipMalloc(&bbin, maxb * 4));
+    CK(hipMalloc(&bfill, maxb * 4));
+    CK(hipMalloc(&nb, 64));
+    hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, 0, in, n);
+    CK(hipDeviceSynchronize());
+    PassArgs a{};
+    a.in.key = in;
+    a.in.pay = nullptr;
+    a.in.n = (long long)n;
+    a.in.form = kPacked64;
+    a.n = n;
+    a.nseg = 1;
+    a.out_rows = out;
+    a.bbin = bbin;
+    a.bfill = bfill;
+    a.nb = nb;
+    a.max_buckets = (unsigned)maxb;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const unsigned grid = pass_grid(n);
+    auto run = [&](const char *name, auto launch) {
+        CK(hipMemset(nb, 0, 4));
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < 5; ++i) {
+            CK(hipMemsetAsync(nb, 0, 4));
+            launch();
+        }
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= 5;
+        printf("%-40s %7.3f ms  %7.1f GB/s (32 B/row)\n", name, ms, 32.0 * n / ms / 1e6);
+    };
+    for (int fb : {9, 8}) {
+        a.fbits = fb;
+        a.shift = 64 - fb;
+        for (int pbl : {9, 8}) {
+            a.out_pbl = pbl;
+            char nm[64];
+#define P(ABL, TXT)                                                                                     \
+    snprintf(nm, sizeof nm, "F%d PB%d %s", 1 << fb, 1 << pbl, TXT);                                     \
+    run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a); })
+            P(0, "full");
+            P(1, "no stores");
+            P(2, "synthetic rows");
+            P(3, "no loads, no stores (LDS only)");
+            P(4, "contiguous stores");
+            P(8, "line-aligned runs");
+#undef P
+        }
+    }
+    return 0;
+}
