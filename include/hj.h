@@ -171,6 +171,22 @@ int hj_dev_join_rows_i32(hj_ctx *ctx, const int32_t *t1, int64_t r1, int64_t c1,
                          int64_t r2, int64_t c2, int64_t ld2, int32_t *out, int64_t ldo, int64_t out_cap,
                          uint64_t *d_count, void *stream);
 
+/* Selection (Experiments/selection.mlir:34-155): the elements v of `in`
+ * with `v <cmp> value`, compacted in input order into out[0 .. min(M,
+ * out_cap)), their source indices into out_row (optional, may be NULL);
+ * d_count = M.  Float compares are ordered: NaN never passes (the reference
+ * uses `cmpf olt`). */
+#define HJ_CMP_LT 0
+#define HJ_CMP_LE 1
+#define HJ_CMP_GT 2
+#define HJ_CMP_GE 3
+#define HJ_CMP_EQ 4
+#define HJ_CMP_NE 5
+int hj_dev_select_f32(hj_ctx *ctx, const float *in, int64_t n, int cmp, float value, float *out, int64_t *out_row,
+                      int64_t out_cap, uint64_t *d_count, void *stream);
+int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_t value, int64_t *out,
+                      int64_t *out_row, int64_t out_cap, uint64_t *d_count, void *stream);
+
 /* ------------------------------------------------------- host memref ABI
  * Two-phase, reference-shaped (mirrors @countRows -> alloc -> @probeRelation,
  * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion.  Both calls
@@ -207,6 +223,13 @@ int64_t hj_join_rows_i32(int32_t *t1_alloc, int32_t *t1_align, int64_t t1_off, i
                          int64_t t2_rows, int64_t t2_cols, int64_t t2_s0, int64_t t2_s1, int32_t *o_alloc,
                          int32_t *o_align, int64_t o_off, int64_t o_rows, int64_t o_cols, int64_t o_s0,
                          int64_t o_s1);
+
+/* selection.mlir's query over host memrefs: in[i] < value (olt) compacted
+ * into the result memref; returns M, or < 0 (HJ_ERR_CAPACITY if the result
+ * memref is shorter than M). */
+int64_t hj_select_f32(float *in_alloc, float *in_align, int64_t in_off, int64_t in_size, int64_t in_stride,
+                      float value, float *out_alloc, float *out_align, int64_t out_off, int64_t out_size,
+                      int64_t out_stride);
 
 /* ------------------------------------------------------ MLIR C-interface
  * Descriptor structs of memref<?xT> / memref<?x2xT> (MLIR's StridedMemRefType

@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "hj.h"
@@ -114,6 +115,7 @@ struct hj_ctx {
     Buf nb, pcur, tile_start, tile_owner, work_start, work_desc, scan_sums;
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
+    Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -441,6 +443,32 @@ int do_join_rows(hj_ctx *c, const RowTables &a, int32_t *out, int64_t ldo, int64
     return HJ_OK;
 }
 
+// Experiments/selection.mlir (:34-155) generalised: survivors of v <op> c,
+// order-preserving, optional source row ids.
+template <class V>
+int do_select(hj_ctx *c, const V *in, int64_t n, int op, V value, V *out, int64_t *out_row, int64_t cap,
+              uint64_t *d_count, hipStream_t st) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (!d_count) HJ_FAIL(HJ_ERR_ARG, "null count pointer");
+    if (n < 0 || (n > 0 && !in)) HJ_FAIL(HJ_ERR_ARG, "bad selection input");
+    if (op < HJ_CMP_LT || op > HJ_CMP_NE) HJ_FAIL(HJ_ERR_ARG, "unknown comparison");
+    if (cap < 0 || (cap > 0 && !out)) HJ_FAIL(HJ_ERR_ARG, "bad selection output");
+    HJ_TRY(set_device(c));
+    const size_t nt = hj::select_tiles(n) + 1;
+    HJ_TRY(ensure_buf(c->sel_tiles, nt * 8));
+    HJ_TRY(ensure_buf(c->sel_sums, hj::exclusive_scan_sums(nt) * 8));
+    hipError_t e;
+    if constexpr (std::is_same<V, float>::value)
+        e = hj::launch_select_f32(in, n, op, value, out, (long long *)out_row, cap, (unsigned long long *)d_count,
+                                  (unsigned long long *)c->sel_tiles.p, (unsigned long long *)c->sel_sums.p, st);
+    else
+        e = hj::launch_select_i64((const long long *)in, n, op, (long long)value, (long long *)out,
+                                  (long long *)out_row, cap, (unsigned long long *)d_count,
+                                  (unsigned long long *)c->sel_tiles.p, (unsigned long long *)c->sel_sums.p, st);
+    HJ_HIP(e);
+    return HJ_OK;
+}
+
 int dbuf(hj_ctx *c, int i, size_t bytes, void **p) {
     if (bytes == 0) bytes = 16;
     if (c->dbuf_bytes[i] < bytes) {
@@ -712,7 +740,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
     for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums,
-                   &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py})
+                   &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums})
         free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -1140,6 +1168,39 @@ void _mlir_ciface_hj_join_rows_i32(hj_memref2_i32 *res, hj_memref2_i32 *t1, hj_m
     res->sizes[1] = oc;
     res->strides[0] = oc;
     res->strides[1] = 1;
+}
+
+// ------------------------------------------------------------- selection
+int hj_dev_select_f32(hj_ctx *c, const float *in, int64_t n, int cmp, float value, float *out, int64_t *out_row,
+                      int64_t out_cap, uint64_t *d_count, void *stream) {
+    return do_select<float>(c, in, n, cmp, value, out, out_row, out_cap, d_count, (hipStream_t)stream);
+}
+
+int hj_dev_select_i64(hj_ctx *c, const int64_t *in, int64_t n, int cmp, int64_t value, int64_t *out,
+                      int64_t *out_row, int64_t out_cap, uint64_t *d_count, void *stream) {
+    return do_select<int64_t>(c, in, n, cmp, value, out, out_row, out_cap, d_count, (hipStream_t)stream);
+}
+
+int64_t hj_select_f32(float *, float *in, int64_t in_off, int64_t in_size, int64_t in_stride, float value, float *,
+                      float *out, int64_t out_off, int64_t out_size, int64_t out_stride) {
+    hj_ctx *c = default_ctx();
+    if (!c) return HJ_ERR_HIP;
+    if (in_size < 0 || out_size < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
+    HJ_TRY(set_device(c));
+    HJ_TRY(host_stream(c));
+    hipStream_t st = c->host_stream;
+    void *din, *dout;
+    HJ_TRY(dbuf(c, 0, sizeof(float) * (size_t)in_size, &din));
+    HJ_TRY(dbuf(c, 1, sizeof(float) * (size_t)(in_size > 0 ? in_size : 1), &dout));
+    HJ_TRY(upload<float>(din, in, in_off, in_size, in_stride, st));
+    HJ_TRY(do_select<float>(c, (const float *)din, in_size, HJ_CMP_LT, value, (float *)dout, nullptr, in_size,
+                            (uint64_t *)c->dcount, st));
+    uint64_t m = 0;
+    HJ_HIP(hipMemcpyAsync(&m, c->dcount, 8, hipMemcpyDeviceToHost, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    if ((int64_t)m > out_size) HJ_FAIL(HJ_ERR_CAPACITY, "result memref smaller than the selection");
+    HJ_TRY(download<float>(out, out_off, (int64_t)m, out_stride, dout, st));
+    return (int64_t)m;
 }
 
 void hj_free_result(void *allocated) { std::free(allocated); }

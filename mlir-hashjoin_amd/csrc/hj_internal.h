@@ -127,6 +127,20 @@ hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
                             hipStream_t st);
 
+// exclusive scan of a u64 array in place (hj_radix.hip); sums >= exclusive_scan_sums(len)
+hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,
+                              hipStream_t st);
+size_t exclusive_scan_sums(unsigned long long len);
+
+// selection (hj_kernels.hip): tiles >= select_tiles(n) + 1 words, sums >= exclusive_scan_sums(tiles)
+size_t select_tiles(long long n);
+hipError_t launch_select_f32(const float *in, long long n, int op, float c, float *out, long long *out_row,
+                             long long cap, unsigned long long *count, unsigned long long *tiles,
+                             unsigned long long *sums, hipStream_t st);
+hipError_t launch_select_i64(const long long *in, long long n, int op, long long c, long long *out,
+                             long long *out_row, long long cap, unsigned long long *count, unsigned long long *tiles,
+                             unsigned long long *sums, hipStream_t st);
+
 // nested-loop.mlir result rows (hj_kernels.hip)
 hipError_t launch_key_col_i32(const int *t, long long rows, long long ld, int *out, hipStream_t st);
 hipError_t launch_gather_rows_i32(const int *x, long long ldx, int cx, const int *y, long long ldy, int cy,

@@ -556,6 +556,101 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows_i32(const int *x, long l
     }
 }
 
+// ------------------------------------------------------------------ selection
+// Experiments/selection.mlir (:34-155): keep the elements that pass
+// `v <op> c`, compacted.  Order-preserving here (the reference orders blocks
+// by an atomic): count per 4096-element tile, exclusive scan of the counts,
+// then each tile writes its survivors with wave ballots in element order.
+// Float compares are ordered (NaN never passes), like the reference's olt.
+constexpr int kSelItems = 16;
+constexpr int kSelTile = kBlock * kSelItems;
+
+template <typename V>
+__device__ __forceinline__ bool sel_pass(V v, int op, V c) {
+    switch (op) {
+        case 0: return v < c;
+        case 1: return v <= c;
+        case 2: return v > c;
+        case 3: return v >= c;
+        case 4: return v == c;
+        default: return v < c || v > c;   // ordered not-equal
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kBlock) void k_sel_count(const V *in, long long n, int op, V c,
+                                                      unsigned long long *tile_cnt) {
+    __shared__ unsigned ws[kBlock / 64];
+    const long long base = (long long)blockIdx.x * kSelTile + threadIdx.x;
+    unsigned k = 0;
+#pragma unroll
+    for (int i = 0; i < kSelItems; ++i) {
+        const long long e = base + (long long)i * kBlock;
+        k += (e < n && sel_pass(in[e], op, c)) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) k += __shfl_down(k, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = k;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned t = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+        tile_cnt[blockIdx.x] = t;
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kBlock) void k_sel_write(const V *in, long long n, int op, V c,
+                                                      const unsigned long long *tile_off, unsigned ntiles, V *out,
+                                                      long long *out_row, long long cap,
+                                                      unsigned long long *count) {
+    constexpr int NW = kBlock / 64;
+    __shared__ unsigned s_cw[kSelItems * NW];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long long base = (long long)blockIdx.x * kSelTile + threadIdx.x;
+    V v[kSelItems];
+    unsigned pass = 0;
+#pragma unroll
+    for (int i = 0; i < kSelItems; ++i) {
+        const long long e = base + (long long)i * kBlock;
+        v[i] = e < n ? in[e] : V(0);
+        if (e < n && sel_pass(v[i], op, c)) pass |= 1u << i;
+    }
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    unsigned lpre[kSelItems];
+#pragma unroll
+    for (int i = 0; i < kSelItems; ++i) {
+        const unsigned long long bal = __ballot((pass >> i) & 1u);
+        lpre[i] = (unsigned)__popcll(bal & lt);
+        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+    }
+    __syncthreads();
+    if (wv == 0) {   // element order = (slot i, wave, lane): scan the 64 run lengths
+        static_assert(kSelItems * NW == 64, "one lane per run");
+        const unsigned x0 = s_cw[lane];
+        unsigned x = x0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        s_cw[lane] = x - x0;
+    }
+    __syncthreads();
+    const unsigned long long tb = tile_off[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kSelItems; ++i) {
+        if (!((pass >> i) & 1u)) continue;
+        const unsigned long long g = tb + s_cw[i * NW + wv] + lpre[i];
+        if (g < (unsigned long long)cap) {
+            out[g] = v[i];
+            if (out_row) out_row[g] = base + (long long)i * kBlock;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = tile_off[ntiles];
+}
+
 inline unsigned grid_for(long long n, int per_block) {
     return (unsigned)((n + per_block - 1) / per_block);
 }
@@ -691,6 +786,36 @@ hipError_t launch_gather_rows_i32(const int *x, long long ldx, int cx, const int
     hipLaunchKernelGGL(k_gather_rows_i32, dim3(g), dim3(kBlock), 0, st, x, ldx, cx, y, ldy, cy, px, py, count, cap,
                        out, ldo);
     return hipGetLastError();
+}
+
+size_t select_tiles(long long n) { return (size_t)(n > 0 ? (n + kSelTile - 1) / kSelTile : 0); }
+
+template <typename V>
+static hipError_t launch_select_t(const V *in, long long n, int op, V c, V *out, long long *out_row, long long cap,
+                                  unsigned long long *count, unsigned long long *tiles, unsigned long long *sums,
+                                  hipStream_t st) {
+    const unsigned nt = (unsigned)select_tiles(n);
+    if (nt == 0) return hipMemsetAsync(count, 0, sizeof(unsigned long long), st);
+    hipLaunchKernelGGL((k_sel_count<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c, tiles);
+    hipError_t e = hipMemsetAsync(tiles + nt, 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    e = exclusive_scan_u64(tiles, (unsigned long long)nt + 1, sums, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((k_sel_write<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c,
+                       (const unsigned long long *)tiles, nt, out, out_row, cap, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_f32(const float *in, long long n, int op, float c, float *out, long long *out_row,
+                             long long cap, unsigned long long *count, unsigned long long *tiles,
+                             unsigned long long *sums, hipStream_t st) {
+    return launch_select_t<float>(in, n, op, c, out, out_row, cap, count, tiles, sums, st);
+}
+
+hipError_t launch_select_i64(const long long *in, long long n, int op, long long c, long long *out,
+                             long long *out_row, long long cap, unsigned long long *count, unsigned long long *tiles,
+                             unsigned long long *sums, hipStream_t st) {
+    return launch_select_t<long long>(in, n, op, c, out, out_row, cap, count, tiles, sums, st);
 }
 
 }  // namespace hj

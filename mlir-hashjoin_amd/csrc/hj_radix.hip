@@ -1006,6 +1006,15 @@ unsigned long long radix_tiles(long long n, int max_nseg) {
 
 size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
 
+hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,
+                              hipStream_t st) {
+    if (len == 0) return hipSuccess;
+    scan_u64(v, len, sums, st);
+    return hipGetLastError();
+}
+
+size_t exclusive_scan_sums(unsigned long long len) { return (size_t)(len / kScanBlock + 2); }
+
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets) {
     const JoinVariant jv = join_variant();
     const u64 chb = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kFinalPbl);

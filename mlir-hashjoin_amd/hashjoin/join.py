@@ -219,6 +219,25 @@ class HashJoin:
               "hj_dev_join_rows_i32")
         return out[:m]
 
+    CMP = {"lt": 0, "le": 1, "gt": 2, "ge": 3, "eq": 4, "ne": 5}
+
+    def select(self, values, op, value, with_rows=False, stream=None):
+        """Experiments/selection.mlir's query on device: the elements v of a
+        float32 or int64 tensor with `v <op> value` ('lt' 'le' 'gt' 'ge' 'eq'
+        'ne'), compacted in input order (and their indices if with_rows)."""
+        _need_cuda(values)
+        if values.dtype not in (torch.float32, torch.int64) or values.dim() != 1:
+            raise ValueError("selection input must be a 1-D float32 or int64 tensor")
+        n = values.numel()
+        out = torch.empty(max(n, 1), dtype=values.dtype, device=values.device)
+        rows = torch.empty(max(n, 1), dtype=torch.int64, device=values.device) if with_rows else None
+        f = lib.hj_dev_select_f32 if values.dtype == torch.float32 else lib.hj_dev_select_i64
+        v = float(value) if values.dtype == torch.float32 else int(value)
+        check(f(self._ctx, _ptr(values), n, self.CMP[op], v, _ptr(out), _ptr(rows) if with_rows else None, n,
+                _ptr(self._count), _stream(self.device, stream)), "hj_dev_select")
+        m = int(self._count.item())
+        return (out[:m], rows[:m]) if with_rows else out[:m]
+
     def join(self, rkey, rpay, skey, spay=None, capacity=None, stream=None):
         """The @main join (join_v2.mlir:646-696) on device tensors: build, then
         probe into an output sized optimistically (|S| rows, or `capacity`),

@@ -102,6 +102,11 @@ def ciface_join_rows_i32(t1, t2):
     return out
 
 
+def select_f32(a, value, out, a_base=None, out_base=None):
+    """selection.mlir over host memrefs: a[i] < value compacted into `out`; returns M."""
+    return int(lib.hj_select_f32(*expand(a, a_base), C.c_float(value), *expand(out, out_base)))
+
+
 def _desc1(a, cls):
     d = cls()
     ct = _CT[a.dtype]

@@ -506,6 +506,63 @@ int64_t oracle_nested_join_rows_i32(const int32_t *t1, int64_t r1, int64_t c1,
     return w;
 }
 
+/* Experiments/selection.mlir @run_selection (:34-155), serialised: keep
+ * d_arrayA[i] when the predicate holds (`cmpf olt` against %compare_val,
+ * :69-70; generalised to op 0..5 = lt le gt ge eq ne, float compares
+ * ordered), written in element order (one legal order of the reference's
+ * per-block atomic offsets, :120-124).  Returns the count; writes at most
+ * cap values (and their indices into rows, if non-NULL). */
+int64_t oracle_select_f32(const float *a, int64_t n, int op, float c, float *out, int64_t *rows, int64_t cap) {
+    int64_t w = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const float v = a[i];
+        int keep;
+        switch (op) {
+            case 0: keep = v < c; break;
+            case 1: keep = v <= c; break;
+            case 2: keep = v > c; break;
+            case 3: keep = v >= c; break;
+            case 4: keep = v == c; break;
+            default: keep = v < c || v > c; break;
+        }
+        if (!keep) continue;
+        if (w < cap) {
+            if (out) out[w] = v;
+            if (rows) rows[w] = i;
+        }
+        ++w;
+    }
+    return w;
+}
+
+int64_t oracle_select_i64(const int64_t *a, int64_t n, int op, int64_t c, int64_t *out, int64_t *rows, int64_t cap) {
+    int64_t w = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t v = a[i];
+        int keep;
+        switch (op) {
+            case 0: keep = v < c; break;
+            case 1: keep = v <= c; break;
+            case 2: keep = v > c; break;
+            case 3: keep = v >= c; break;
+            case 4: keep = v == c; break;
+            default: keep = v != c; break;
+        }
+        if (!keep) continue;
+        if (w < cap) {
+            if (out) out[w] = v;
+            if (rows) rows[w] = i;
+        }
+        ++w;
+    }
+    return w;
+}
+
+/* selection.mlir @init (:20-29): arr[i] = (float)i */
+void oracle_selection_init_f32(float *a, int64_t n) {
+    for (int64_t i = 0; i < n; ++i) a[i] = (float)(int32_t)i;
+}
+
 /* nested-loop.mlir @init (:7-24): t[i][j] = i + j */
 void oracle_nested_init_i32(int32_t *t, int64_t rows, int64_t cols) {
     for (int64_t i = 0; i < rows; ++i)

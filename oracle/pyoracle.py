@@ -72,6 +72,12 @@ def lib():
         L.oracle_nested_join_rows_i32.argtypes = [C.c_void_p, _i64, _i64, C.c_void_p, _i64, _i64, C.c_void_p, _i64]
         L.oracle_nested_init_i32.restype = None
         L.oracle_nested_init_i32.argtypes = [C.c_void_p, _i64, _i64]
+        L.oracle_select_f32.restype = _i64
+        L.oracle_select_f32.argtypes = [C.c_void_p, _i64, C.c_int, C.c_float, C.c_void_p, C.c_void_p, _i64]
+        L.oracle_select_i64.restype = _i64
+        L.oracle_select_i64.argtypes = [C.c_void_p, _i64, C.c_int, _i64, C.c_void_p, C.c_void_p, _i64]
+        L.oracle_selection_init_f32.restype = None
+        L.oracle_selection_init_f32.argtypes = [C.c_void_p, _i64]
         L.oracle_pair_digest_i64.restype = None
         L.oracle_pair_digest_i64.argtypes = [C.c_void_p, C.c_void_p, _i64, C.POINTER(_u64), C.POINTER(_u64)]
         _lib = L
@@ -211,6 +217,28 @@ def nested_init_i32(rows, cols):
     t = np.empty((rows, cols), np.int32)
     lib().oracle_nested_init_i32(_p(t), rows, cols)
     return t
+
+
+CMP = {"lt": 0, "le": 1, "gt": 2, "ge": 3, "eq": 4, "ne": 5}
+
+
+def select(a, op, c):
+    """selection.mlir restated: (values, row indices) of a[i] <op> c, in order."""
+    L = lib()
+    if a.dtype == np.float32:
+        a = np.ascontiguousarray(a); f = L.oracle_select_f32; c = float(c)
+    else:
+        a = np.ascontiguousarray(a, np.int64); f = L.oracle_select_i64; c = int(c)
+    m = f(_p(a), len(a), CMP[op], c, None, None, 0)
+    out = np.empty(max(m, 1), a.dtype); rows = np.empty(max(m, 1), np.int64)
+    f(_p(a), len(a), CMP[op], c, _p(out), _p(rows), m)
+    return out[:m], rows[:m]
+
+
+def selection_init_f32(n):
+    a = np.empty(n, np.float32)
+    lib().oracle_selection_init_f32(_p(a), n)
+    return a
 
 
 def pair_digest(r, s):

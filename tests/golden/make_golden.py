@@ -113,6 +113,14 @@ def main():
     assert np.array_equal(rows, kat)
     np.savez_compressed(os.path.join(HERE, "nested_loop_kat.npz"), t1=t1, t2=t2, rows=rows)
     print("nested_loop_kat: 20 rows (hand-derived from nested-loop.mlir semantics)")
+    # Experiments/selection.mlir @main (:159-193): 128 elements arr[i] = i,
+    # predicate arr[i] < 80.0 -> 80 values 0..79 (hand-derived)
+    a = O.selection_init_f32(128)
+    vals, rows = O.select(a, "lt", 80.0)
+    assert np.array_equal(vals, np.arange(80, dtype=np.float32)) and np.array_equal(rows, np.arange(80))
+    np.savez_compressed(os.path.join(HERE, "selection_kat.npz"), input=a, value=np.float32(80.0), values=vals,
+                        rows=rows)
+    print("selection_kat: 80 of 128 (hand-derived from selection.mlir semantics)")
 
 
 if __name__ == "__main__":

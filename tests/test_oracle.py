@@ -110,3 +110,31 @@ def test_pair_digest_order_independent(oracle):
     p = rng.permutation(1000)
     assert oracle.pair_digest(r, s) == oracle.pair_digest(r[p], s[p])
     assert oracle.pair_digest(r, s) != oracle.pair_digest(s, r)
+
+
+def test_selection_kat(oracle):
+    """selection.mlir @main: arr[i] = i (128), keep arr[i] < 80.0 -> 0..79."""
+    with np.load(os.path.join(GOLDEN, "selection_kat.npz"), allow_pickle=False) as z:
+        a, c, vals, rows = z["input"], float(z["value"]), z["values"], z["rows"]
+    assert np.array_equal(a, oracle.selection_init_f32(128))
+    v, r = oracle.select(a, "lt", c)
+    assert np.array_equal(v, vals) and np.array_equal(r, rows)
+
+
+def test_selection_semantics(oracle):
+    """Ordered float compares (NaN never selected); every op against numpy."""
+    rng = np.random.default_rng(3)
+    a = rng.normal(size=5000).astype(np.float32)
+    a[::17] = np.nan; a[::29] = np.inf; a[::31] = -np.inf; a[::37] = 0.25
+    ops = {"lt": np.less, "le": np.less_equal, "gt": np.greater, "ge": np.greater_equal, "eq": np.equal}
+    for op, f in ops.items():
+        v, r = oracle.select(a, op, 0.25)
+        keep = np.nonzero(f(a, np.float32(0.25)))[0]
+        assert np.array_equal(r, keep) and np.array_equal(v, a[keep])
+    v, r = oracle.select(a, "ne", 0.25)
+    keep = np.nonzero((a < 0.25) | (a > 0.25))[0]   # ordered: NaN excluded
+    assert np.array_equal(r, keep)
+    k = rng.integers(-50, 50, 3000)
+    for op, f in list(ops.items()) + [("ne", np.not_equal)]:
+        v, r = oracle.select(k, op, 7)
+        assert np.array_equal(r, np.nonzero(f(k, 7))[0])
