@@ -559,11 +559,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows_i32(const int *x, long l
 // ------------------------------------------------------------------ selection
 // Experiments/selection.mlir (:34-155): keep the elements that pass
 // `v <op> c`, compacted.  Order-preserving here (the reference orders blocks
-// by an atomic): count per 4096-element tile, exclusive scan of the counts,
-// then each tile writes its survivors with wave ballots in element order.
+// by an atomic): count per tile, exclusive scan of the counts, then each tile
+// writes its survivors in element order.  A lane reads 16 B per load: slot j
+// of lane t holds elements j*64*NW*W + t*W .. +W (W = 16 B / sizeof(V)), so
+// element order is (slot, wave, lane, w) and positions come from per-lane
+// counts, a wave prefix sum and one (slot, wave) scan per tile.
 // Float compares are ordered (NaN never passes), like the reference's olt.
-constexpr int kSelItems = 16;
-constexpr int kSelTile = kBlock * kSelItems;
+constexpr int kSelSlots = 4;
 
 template <typename V>
 __device__ __forceinline__ bool sel_pass(V v, int op, V c) {
@@ -578,15 +580,39 @@ __device__ __forceinline__ bool sel_pass(V v, int op, V c) {
 }
 
 template <typename V>
-__global__ __launch_bounds__(kBlock) void k_sel_count(const V *in, long long n, int op, V c,
+struct SelVec {
+    static constexpr int W = 16 / sizeof(V);
+    static constexpr long long kTile = (long long)kBlock * kSelSlots * W;
+    V v[W];
+};
+
+// Slot j of this lane: W elements at e0 (vector load when whole and aligned).
+template <typename V>
+__device__ __forceinline__ void sel_load(const V *in, long long n, long long e0, bool vec_ok, SelVec<V> &x) {
+    constexpr int W = SelVec<V>::W;
+    if (vec_ok && e0 + W <= n) {
+        const uint4 u = *(const uint4 *)(in + e0);
+        __builtin_memcpy(x.v, &u, 16);
+    } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w) x.v[w] = e0 + w < n ? in[e0 + w] : V(0);
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(kBlock) void k_sel_count(const V *in, long long n, int op, V c, bool vec_ok,
                                                       unsigned long long *tile_cnt) {
+    constexpr int W = SelVec<V>::W;
     __shared__ unsigned ws[kBlock / 64];
-    const long long base = (long long)blockIdx.x * kSelTile + threadIdx.x;
+    const long long base = (long long)blockIdx.x * SelVec<V>::kTile + (long long)threadIdx.x * W;
     unsigned k = 0;
 #pragma unroll
-    for (int i = 0; i < kSelItems; ++i) {
-        const long long e = base + (long long)i * kBlock;
-        k += (e < n && sel_pass(in[e], op, c)) ? 1u : 0u;
+    for (int j = 0; j < kSelSlots; ++j) {
+        SelVec<V> x;
+        const long long e0 = base + (long long)j * kBlock * W;
+        sel_load(in, n, e0, vec_ok, x);
+#pragma unroll
+        for (int w = 0; w < W; ++w) k += (e0 + w < n && sel_pass(x.v[w], op, c)) ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) k += __shfl_down(k, o, 64);
@@ -601,51 +627,60 @@ __global__ __launch_bounds__(kBlock) void k_sel_count(const V *in, long long n, 
 }
 
 template <typename V>
-__global__ __launch_bounds__(kBlock) void k_sel_write(const V *in, long long n, int op, V c,
+__global__ __launch_bounds__(kBlock) void k_sel_write(const V *in, long long n, int op, V c, bool vec_ok,
                                                       const unsigned long long *tile_off, unsigned ntiles, V *out,
                                                       long long *out_row, long long cap,
                                                       unsigned long long *count) {
+    constexpr int W = SelVec<V>::W;
     constexpr int NW = kBlock / 64;
-    __shared__ unsigned s_cw[kSelItems * NW];
+    __shared__ unsigned s_cw[kSelSlots * NW];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const long long base = (long long)blockIdx.x * kSelTile + threadIdx.x;
-    V v[kSelItems];
-    unsigned pass = 0;
+    const long long base = (long long)blockIdx.x * SelVec<V>::kTile + (long long)threadIdx.x * W;
+    SelVec<V> x[kSelSlots];
+    unsigned pass[kSelSlots], lpre[kSelSlots];
 #pragma unroll
-    for (int i = 0; i < kSelItems; ++i) {
-        const long long e = base + (long long)i * kBlock;
-        v[i] = e < n ? in[e] : V(0);
-        if (e < n && sel_pass(v[i], op, c)) pass |= 1u << i;
-    }
-    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    unsigned lpre[kSelItems];
+    for (int j = 0; j < kSelSlots; ++j) {
+        const long long e0 = base + (long long)j * kBlock * W;
+        sel_load(in, n, e0, vec_ok, x[j]);
+        pass[j] = 0;
 #pragma unroll
-    for (int i = 0; i < kSelItems; ++i) {
-        const unsigned long long bal = __ballot((pass >> i) & 1u);
-        lpre[i] = (unsigned)__popcll(bal & lt);
-        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
-    }
-    __syncthreads();
-    if (wv == 0) {   // element order = (slot i, wave, lane): scan the 64 run lengths
-        static_assert(kSelItems * NW == 64, "one lane per run");
-        const unsigned x0 = s_cw[lane];
-        unsigned x = x0;
+        for (int w = 0; w < W; ++w)
+            if (e0 + w < n && sel_pass(x[j].v[w], op, c)) pass[j] |= 1u << w;
+        // lane prefix within the wave for this slot
+        const unsigned k = (unsigned)__popc(pass[j]);
+        unsigned xs = k;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const unsigned y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
+            const unsigned y = __shfl_up(xs, o, 64);
+            if (lane >= o) xs += y;
         }
-        s_cw[lane] = x - x0;
+        lpre[j] = xs - k;
+        if (lane == 63) s_cw[j * NW + wv] = xs;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // (slot, wave) runs in element order: kSelSlots * NW = 16 entries
+        unsigned run = 0;
+#pragma unroll
+        for (int q = 0; q < kSelSlots * NW; ++q) {
+            const unsigned v = s_cw[q];
+            s_cw[q] = run;
+            run += v;
+        }
     }
     __syncthreads();
     const unsigned long long tb = tile_off[blockIdx.x];
 #pragma unroll
-    for (int i = 0; i < kSelItems; ++i) {
-        if (!((pass >> i) & 1u)) continue;
-        const unsigned long long g = tb + s_cw[i * NW + wv] + lpre[i];
-        if (g < (unsigned long long)cap) {
-            out[g] = v[i];
-            if (out_row) out_row[g] = base + (long long)i * kBlock;
+    for (int j = 0; j < kSelSlots; ++j) {
+        unsigned long long g = tb + s_cw[j * NW + wv] + lpre[j];
+        const long long e0 = base + (long long)j * kBlock * W;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            if (!((pass[j] >> w) & 1u)) continue;
+            if (g < (unsigned long long)cap) {
+                out[g] = x[j].v[w];
+                if (out_row) out_row[g] = e0 + w;
+            }
+            ++g;
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *count = tile_off[ntiles];
@@ -788,20 +823,25 @@ hipError_t launch_gather_rows_i32(const int *x, long long ldx, int cx, const int
     return hipGetLastError();
 }
 
-size_t select_tiles(long long n) { return (size_t)(n > 0 ? (n + kSelTile - 1) / kSelTile : 0); }
+static size_t select_tiles_of(long long n, long long tile) { return (size_t)(n > 0 ? (n + tile - 1) / tile : 0); }
+
+size_t select_tiles(long long n) {   // upper bound over element types (int64 tiles hold fewer elements)
+    return select_tiles_of(n, SelVec<long long>::kTile);
+}
 
 template <typename V>
 static hipError_t launch_select_t(const V *in, long long n, int op, V c, V *out, long long *out_row, long long cap,
                                   unsigned long long *count, unsigned long long *tiles, unsigned long long *sums,
                                   hipStream_t st) {
-    const unsigned nt = (unsigned)select_tiles(n);
+    const unsigned nt = (unsigned)select_tiles_of(n, SelVec<V>::kTile);
     if (nt == 0) return hipMemsetAsync(count, 0, sizeof(unsigned long long), st);
-    hipLaunchKernelGGL((k_sel_count<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c, tiles);
+    const bool vec_ok = (((uintptr_t)in) & 15) == 0;
+    hipLaunchKernelGGL((k_sel_count<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c, vec_ok, tiles);
     hipError_t e = hipMemsetAsync(tiles + nt, 0, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     e = exclusive_scan_u64(tiles, (unsigned long long)nt + 1, sums, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_sel_write<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c,
+    hipLaunchKernelGGL((k_sel_write<V>), dim3(nt), dim3(kBlock), 0, st, in, n, op, c, vec_ok,
                        (const unsigned long long *)tiles, nt, out, out_row, cap, count);
     return hipGetLastError();
 }
