@@ -187,6 +187,18 @@ int hj_dev_select_f32(hj_ctx *ctx, const float *in, int64_t n, int cmp, float va
 int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_t value, int64_t *out,
                       int64_t *out_row, int64_t out_cap, uint64_t *d_count, void *stream);
 
+/* Out-of-core join of HOST-resident int64 key/payload columns (relations
+ * larger than HBM; the reference leaves the partitioned join out,
+ * projectDescription.md:23-24).  When R does not fit device_budget bytes
+ * (0 = 80 % of free HBM), R and S are routed by hj_partition_of into groups
+ * that do, through the GPU in chunks; each group is built on the GPU and its
+ * S side streamed through the probe with copies overlapping the probe.
+ * Pairs (R.pay, S.pay) go to out_r/out_s (host); returns M (rows past
+ * out_cap dropped) or < 0. */
+int64_t hj_host_join_ooc_i64(hj_ctx *ctx, const int64_t *rkey, const int64_t *rpay, int64_t nr, const int64_t *skey,
+                             const int64_t *spay, int64_t ns, int64_t *out_r, int64_t *out_s, int64_t out_cap,
+                             uint64_t device_budget);
+
 /* ------------------------------------------------------- host memref ABI
  * Two-phase, reference-shaped (mirrors @countRows -> alloc -> @probeRelation,
  * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion.  Both calls

@@ -87,6 +87,7 @@ def _load():
         "hj_count_rows_i32": (_i64, [_vp, _vp, _i64, _i64, _i64, _i64, _i64] * 2),
         "hj_join_rows_i32": (_i64, [_vp, _vp, _i64, _i64, _i64, _i64, _i64] * 3),
         "_mlir_ciface_hj_join_rows_i32": (None, [_vp, _vp, _vp]),
+        "hj_host_join_ooc_i64": (_i64, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _u64]),
         "hj_dev_select_f32": (_int, [_vp, _vp, _i64, _int, C.c_float, _vp, _vp, _i64, _vp, _vp]),
         "hj_dev_select_i64": (_int, [_vp, _vp, _i64, _int, _i64, _vp, _vp, _i64, _vp, _vp]),
         "hj_select_f32": (_i64, [_vp, _vp, _i64, _i64, _i64, C.c_float, _vp, _vp, _i64, _i64, _i64]),

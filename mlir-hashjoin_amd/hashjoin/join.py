@@ -219,6 +219,28 @@ class HashJoin:
               "hj_dev_join_rows_i32")
         return out[:m]
 
+    def join_host(self, rkey, rpay, skey, spay, device_budget=0, capacity=None):
+        """Out-of-core join of host-resident int64 numpy columns (relations
+        larger than HBM): routed into groups that fit `device_budget` bytes
+        (0 = 80 % of free HBM), each built on the GPU with its probe side
+        streamed through.  Returns host arrays (R.pay, S.pay)."""
+        import numpy as np
+        cols = [np.ascontiguousarray(a, np.int64) for a in (rkey, rpay, skey, spay)]
+        if cols[0].shape != cols[1].shape or cols[2].shape != cols[3].shape:
+            raise ValueError("key and payload columns must have equal lengths")
+        cap = max(1, cols[2].size if capacity is None else int(capacity))
+        for _ in range(2):
+            out_r = np.empty(cap, np.int64); out_s = np.empty(cap, np.int64)
+            m = lib.hj_host_join_ooc_i64(self._ctx, cols[0].ctypes.data, cols[1].ctypes.data, cols[0].size,
+                                         cols[2].ctypes.data, cols[3].ctypes.data, cols[2].size,
+                                         out_r.ctypes.data, out_s.ctypes.data, cap, int(device_budget))
+            if m < 0:
+                check(int(m), "hj_host_join_ooc_i64")
+            if m <= cap:
+                return out_r[:m], out_s[:m]
+            cap = int(m)
+        raise RuntimeError("out-of-core join output did not fit after resizing")
+
     CMP = {"lt": 0, "le": 1, "gt": 2, "ge": 3, "eq": 4, "ne": 5}
 
     def select(self, values, op, value, with_rows=False, stream=None):
