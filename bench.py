@@ -124,7 +124,7 @@ def main():
     expect_m = NS if distn in ("pkfk", "zipf") else None
     torch.cuda.synchronize()
 
-    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0,
+    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0, "route": 0.0,
               "partition+exchange": 0.0}
     last = {}
 
@@ -155,10 +155,13 @@ def main():
             o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev)
             ev["probed"].synchronize()
             if acc:
-                phases["partition+exchange"] += ev["start"].elapsed_time(ev["exchanged"])
-                phases["build"] += ev["exchanged"].elapsed_time(ev["built"])
+                # transfers overlap compute (hashjoin.dist): R's tuples move
+                # during S's routing, S's during R's build
+                phases["route"] += ev["start"].elapsed_time(ev["routed"])
+                phases["build"] += ev["routed"].elapsed_time(ev["built"])
                 phases["probe"] += ev["built"].elapsed_time(ev["probed"])
             last["m"] = o_r.numel()
+            last["rows"] = ev["rows"]
             last["out"] = (o_r, o_s)
 
     for _ in range(a.warmup):
@@ -203,7 +206,13 @@ def main():
     join_ms = phases["probe_join"] / a.steps
     build_ms = (phases["init"] + phases["build"]) / a.steps
     strategy = hj.strategy_used or a.strategy
-    if strategy == "radix":
+    if use_dist:
+        # per-kernel events are not recorded through the distributed path:
+        # the probe phase (S partition + k_join on the received tuples)
+        nr_loc, ns_loc = last["rows"]
+        kern, join_ms = "probe phase (local S partition + k_join)", probe_ms
+        kbytes = (nr_loc + ns_loc) * 16 + m_local * 16
+    elif strategy == "radix":
         kern, kbytes = "k_join", (nr + ns) * 16 + m_local * 16
     else:
         kern, kbytes = "k_probe", ns * 32 + m_local * 16
@@ -232,7 +241,7 @@ def main():
         "phase_ms": ph,
         "strategy": strategy,
         "roofline": {
-            "kernel": f"{kern} ({'hj_radix.hip' if kern == 'k_join' else 'hj_kernels.hip'})",
+            "kernel": kern if use_dist else f"{kern} ({'hj_radix.hip' if kern == 'k_join' else 'hj_kernels.hip'})",
             "bound": "hbm",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,

@@ -6,9 +6,10 @@ Hash-Join" as left out); north_star adds this path:
 
   1. every rank radix-partitions its slice of R and of S by the owner hash
      (hj_dev_partition_*: one HIP histogram + scatter pass each),
-  2. ONE all-to-all of the per-owner counts (2 x world int64),
-  3. one all-to-all-v of packed 16-B {key, payload} tuples for R and one for
-     S (RCCL grouped send/recv under torch's all_to_all_single),
+  2. per relation, one all-to-all of the per-owner counts (world int64),
+  3. per relation, one batched group of point-to-point messages (RCCL
+     grouped send/recv) of packed 16-B {key, payload} tuples, started
+     asynchronously: R's transfer overlaps S's routing, S's overlaps R's build,
   4. local build + probe on the received tuples (hj_dev_*_tuples_i64).
 
 The output stays distributed: rank p holds the pairs whose key it owns.
@@ -45,7 +46,8 @@ def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows):
     """recv[rows from p] <- every p's send[rows for me]: one batched group of
     point-to-point messages of at most max_rows rows each (views, no staging
     copies).  Sender and receiver cut a slice into the same pieces because
-    in_rows on p and out_rows here describe the same slice."""
+    in_rows on p and out_rows here describe the same slice.  Returns the
+    outstanding works (wait on them before reading recv)."""
     world = len(in_rows)
     me = dist.get_rank(group)
     in_off = [sum(in_rows[:p]) for p in range(world)]
@@ -63,9 +65,36 @@ def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows):
         for a in range(0, out_rows[fr], max_rows):
             b = min(out_rows[fr], a + max_rows)
             ops.append(dist.P2POp(dist.irecv, recv[out_off[fr] + a:out_off[fr] + b], peer_fr, group))
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+class Exchange:
+    """One routed tuple buffer in flight: counts are exchanged at start
+    (blocking: they size the receive buffer), the tuples move asynchronously
+    (batched point-to-point on the backend's stream).  `wait()` orders the
+    current stream after the transfer; `recv` is valid from then on."""
+
+    def __init__(self, send, counts, group=None, max_rows=None):
+        world = dist.get_world_size(group)
+        if counts.numel() != world:
+            raise ValueError("one count per rank required")
+        max_rows = MAX_ROWS_PER_ROUND if max_rows is None else int(max_rows)
+        if max_rows < 1:
+            raise ValueError("max_rows must be positive")
+        counts = counts.contiguous()
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts, group=group)
+        host = torch.stack([counts, recv_counts]).cpu()
+        self.in_rows, self.out_rows = host[0].tolist(), host[1].tolist()
+        self.send = send   # kept alive until the transfer is done
+        self.recv = torch.empty((sum(self.out_rows), 2), dtype=torch.int64, device=send.device)
+        self._works = _all_to_all_rows(self.recv, send, self.out_rows, self.in_rows, group, max_rows)
+
+    def wait(self):
+        for w in self._works:
             w.wait()
+        self._works = []
+        return self.recv
 
 
 def exchange(send_r, counts_r, send_s, counts_s, group=None, max_rows=None):
@@ -74,24 +103,11 @@ def exchange(send_r, counts_r, send_s, counts_s, group=None, max_rows=None):
     send_x: (n, 2) int64 rows grouped by destination rank 0..P-1;
     counts_x: (P,) int64 rows per destination.  Returns (recv_r, recv_s, splits)
     where recv_x holds the rows every rank routed here (grouped by source).
-    Slices larger than max_rows (default MAX_ROWS_PER_ROUND) move in rounds."""
-    world = dist.get_world_size(group)
-    if counts_r.numel() != world or counts_s.numel() != world:
-        raise ValueError("one count per rank required")
-    max_rows = MAX_ROWS_PER_ROUND if max_rows is None else int(max_rows)
-    if max_rows < 1:
-        raise ValueError("max_rows must be positive")
-    both = torch.stack([counts_r, counts_s], dim=1).reshape(-1).contiguous()
-    recv_both = torch.empty_like(both)
-    dist.all_to_all_single(recv_both, both, group=group)
-    host = torch.stack([both.view(world, 2), recv_both.view(world, 2)]).cpu()
-    in_r, in_s = host[0, :, 0].tolist(), host[0, :, 1].tolist()
-    out_r, out_s = host[1, :, 0].tolist(), host[1, :, 1].tolist()
-    recv_r = torch.empty((sum(out_r), 2), dtype=torch.int64, device=send_r.device)
-    recv_s = torch.empty((sum(out_s), 2), dtype=torch.int64, device=send_s.device)
-    _all_to_all_rows(recv_r, send_r, out_r, in_r, group, max_rows)
-    _all_to_all_rows(recv_s, send_s, out_s, in_s, group, max_rows)
-    return recv_r, recv_s, {"in_r": in_r, "in_s": in_s, "out_r": out_r, "out_s": out_s}
+    Slices larger than max_rows (default MAX_ROWS_PER_ROUND) move in pieces."""
+    xr = Exchange(send_r, counts_r, group, max_rows)
+    xs = Exchange(send_s, counts_s, group, max_rows)
+    recv_r, recv_s = xr.wait(), xs.wait()
+    return recv_r, recv_s, {"in_r": xr.in_rows, "in_s": xs.in_rows, "out_r": xr.out_rows, "out_s": xs.out_rows}
 
 
 def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None):
@@ -99,22 +115,27 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
 
     hj: a hashjoin.HashJoin on this rank's GPU.  Returns this rank's share of
     the result (out_r, out_s) = (R.pay, S.pay) of every pair whose key this
-    rank owns.  `phases`, if a dict, receives per-phase CUDA events for
-    timing."""
+    rank owns.  Transfers overlap compute: R's tuples move while S is routed,
+    S's while R is built.  `phases`, if a dict, receives CUDA events
+    (start, routed, built, probed) for timing and "rows" = (received R rows,
+    received S rows)."""
     world = dist.get_world_size(group)
     ev = (lambda name: _event(phases, name)) if phases is not None else (lambda name: None)
     ev("start")
-    _dbg("partition", rkey.numel(), skey.numel())
+    _dbg("route", rkey.numel(), skey.numel())
     send_r, cr = hj.partition(rkey, rpay, world)
+    xr = Exchange(send_r, cr, group)
     send_s, cs = hj.partition(skey, spay, world)
-    ev("partitioned")
-    _dbg("exchange", cr.tolist() if _DEBUG else None, cs.tolist() if _DEBUG else None)
-    recv_r, recv_s, _ = exchange(send_r, cr, send_s, cs, group)
-    ev("exchanged")
-    _dbg("build", recv_r.shape[0], recv_s.shape[0])
+    xs = Exchange(send_s, cs, group)
+    ev("routed")
+    recv_r = xr.wait()
+    _dbg("build", recv_r.shape[0])
     hj.build_tuples(recv_r)
     ev("built")
-    _dbg("probe")
+    recv_s = xs.wait()
+    _dbg("probe", recv_s.shape[0])
+    if phases is not None:
+        phases["rows"] = (recv_r.shape[0], recv_s.shape[0])
     cap = max(1, recv_s.shape[0] if capacity is None else int(capacity))
     for _ in range(2):
         out_r = torch.empty(cap, dtype=torch.int64, device=recv_s.device)
