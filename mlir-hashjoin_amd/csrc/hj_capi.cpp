@@ -108,6 +108,7 @@ struct hj_ctx {
     int64_t n_build = 0;
     int strategy = HJ_STRATEGY_AUTO;   // requested
     int radix_bits = 0;                // 0: planner chooses
+    int xcd_mode = -1;                 // global-table probe XCD split: -1 auto, 0 off, 1 on
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
@@ -299,6 +300,38 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     return HJ_OK;
 }
 
+// XCD split of a global-table probe: worth its extra pass when the table is
+// larger than one XCD's 4 MiB L2 but small enough that 1/8 of it mostly fits
+// (<= 128 MiB), and the probe side is large.  HJ_XCD=0 / 1 forces it off / on.
+constexpr size_t kXcdMinTable = 4ull << 20, kXcdMaxTable = 128ull << 20;
+constexpr int64_t kXcdMinRows = 1ll << 22;
+
+hj::RadixPlan xcd_plan() {
+    hj::RadixPlan pl{};
+    pl.passes = 1;
+    pl.bits[0] = 3;   // log2(kXcdGroups)
+    pl.pbl[0] = hj::kXcdPbl;
+    pl.total_bits = 3;
+    return pl;
+}
+
+bool use_xcd_split(const hj_ctx *c, int layout, int64_t n) {
+    static const int env = [] {
+        const char *e = getenv("HJ_XCD");
+        return e ? atoi(e) : -1;
+    }();
+    const int mode = c->xcd_mode >= 0 ? c->xcd_mode : env;
+    if (mode == 0 || n <= 0) return false;
+    if (mode == 1) return true;
+    // automatic: off for now -- the split cuts the probe's fetched bytes 3.4x
+    // (L2 hit 0.24 -> 0.73 at C2) but the probe kernel is bound elsewhere
+    // (row-list indirection + output cursor), so C2 measured 31.1 ms split vs
+    // 26.6 ms plain (profiles/r01_c2_xcd_profile.txt)
+    if (mode < 0) return false;
+    const size_t table = (size_t(1) << c->bits) * (layout == kWide ? 16 : 8);
+    return n >= kXcdMinRows && table > kXcdMinTable && table <= kXcdMaxTable;
+}
+
 int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *out_s, int64_t cap,
              uint64_t *d_count, bool count_only, hipStream_t st) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
@@ -334,6 +367,28 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     out.counter = (unsigned long long *)d_count;
     record(c, kEvProbe0, st);
     HJ_TRY(ensure_buf(c->slow, (hj::probe_tiles(src.n) + 1) * sizeof(unsigned)));
+    if (use_xcd_split(c, layout, src.n)) {
+        // XCD split: route S by the top 3 bits of the slot hash into 8 groups
+        // (one bucket-chaining pass), then workgroup b probes group b % 8 --
+        // its 1/8 of the table stays in one XCD's L2
+        // (profiles/r01_micro_xcd_slices.txt: 66 -> 265 G probes/s at 32 MiB)
+        const bool wide = layout == kWide;
+        const hj::RadixPlan pl = xcd_plan();
+        HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, wide ? 16 : 8, pl));
+        HJ_HIP(hj::radix_partition(src, wide, pl, radix_work(c), bucket_set(c->sset), st));
+        record(c, kEvProbeMid, st);
+        hj::SrcDev xs = src;
+        xs.key = c->sset.rows.p;
+        xs.pay = nullptr;
+        xs.form = hj::kXcdRows;
+        xs.list = (const unsigned long long *)c->sset.blist.p;
+        xs.pstart = (const unsigned long long *)c->sset.pstart.p;
+        HJ_HIP(hj::launch_probe(table_dev(c), layout, xs, out, count_only, (unsigned *)c->slow.p, st));
+        record(c, kEvProbe1, st);
+        c->rec[2] = c->timing;
+        c->rec_mid = c->timing;
+        return HJ_OK;
+    }
     HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, (unsigned *)c->slow.p, st));
     record(c, kEvProbe1, st);
     c->rec[2] = c->timing;
@@ -846,6 +901,13 @@ int hj_ctx_set_radix_bits(hj_ctx *c, int bits) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     if (bits < 0 || bits > 24) HJ_FAIL(HJ_ERR_ARG, "radix bits must be in [0, 24]");
     c->radix_bits = bits;
+    return HJ_OK;
+}
+
+int hj_ctx_set_xcd_split(hj_ctx *c, int mode) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (mode < -1 || mode > 1) HJ_FAIL(HJ_ERR_ARG, "mode must be -1, 0 or 1");
+    c->xcd_mode = mode;
     return HJ_OK;
 }
 

@@ -44,16 +44,23 @@ struct TableDev {
 
 enum Layout : int { kWide = 0, kNarrow = 1 };
 
-// Source forms of a relation on the device.
-enum SrcForm : int { kCols64 = 0, kPacked64 = 1, kCol32 = 2 };
+// Source forms of a relation on the device.  kXcdRows: a probe side already
+// split into 8 groups by the top 3 bits of the table's slot hash (a radix
+// bucket set of 512-row buckets, packed rows as the partition passes write
+// them), probed group g by workgroups b with b % 8 == g.
+enum SrcForm : int { kCols64 = 0, kPacked64 = 1, kCol32 = 2, kXcdRows = 5 };
 
 struct SrcDev {
-    const void *key;    // int64 column, packed {key,pay} tuples, or int32 column
+    const void *key;    // int64 column, packed {key,pay} tuples, int32 column, or bucket rows (kXcdRows)
     const void *pay;    // int64 column (kCols64 only)
     long long n;
     long long row_base; // kCol32: row id = row_base + row
     int form;
+    const unsigned long long *list = nullptr;     // kXcdRows: bucket << 32 | fill, grouped
+    const unsigned long long *pstart = nullptr;   // kXcdRows: 9 group starts into list
 };
+constexpr int kXcdPbl = 9;        // rows per bucket of a kXcdRows probe side (log2)
+constexpr int kXcdGroups = 8;     // one per XCD
 
 struct OutDev {
     void *r;            // int64 or int32 column (R payload / row id)

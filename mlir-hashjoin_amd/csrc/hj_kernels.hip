@@ -163,6 +163,56 @@ __global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
     if (dup) __hip_atomic_store(&t.meta[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ------------------------------------------------------------------ probe tiles
+// A probe tile is kProbeItems * kBlock rows.  Plain sources: tile q = rows
+// [q * kTile, ...).  kXcdRows: tile (g, q) = buckets 4q .. 4q+3 of group g.
+constexpr int kProbeTile = kBlock * kProbeItems;
+constexpr int kXcdTileBuckets = kProbeTile >> kXcdPbl;
+static_assert(kXcdTileBuckets * (1 << kXcdPbl) == kProbeTile, "tile = whole buckets");
+
+template <int L, int FORM>
+__device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned g, unsigned long long q, int i, Tuple &tp) {
+    if constexpr (FORM == kXcdRows) {
+        const unsigned v = (unsigned)i * kBlock + threadIdx.x;
+        const unsigned long long li = src.pstart[g] + q * kXcdTileBuckets + (v >> kXcdPbl);
+        if (li >= src.pstart[g + 1]) return false;
+        const unsigned long long e = src.list[li];
+        const unsigned off = v & ((1u << kXcdPbl) - 1u);
+        if (off >= (unsigned)e) return false;
+        const unsigned long long r = ((e >> 32) << kXcdPbl) + off;
+        if constexpr (L == kWide) {
+            const ulonglong2 x = ((const ulonglong2 *)src.key)[r];
+            tp = Tuple{x.x, x.y};
+        } else {
+            const unsigned long long x = ((const unsigned long long *)src.key)[r];
+            tp = Tuple{x >> 32, x & 0xffffffffull};
+        }
+        return true;
+    } else {
+        const long long row = (long long)q * kProbeTile + (long long)i * kBlock + threadIdx.x;
+        if (row >= src.n) return false;
+        tp = load_src<FORM>(src, row);
+        return true;
+    }
+}
+
+// Tiles of this workgroup: (group, first tile, stride, tile count).
+template <int FORM>
+__device__ __forceinline__ void probe_tiles(const SrcDev &src, unsigned &g, unsigned long long &q0,
+                                            unsigned long long &step, unsigned long long &nt) {
+    if constexpr (FORM == kXcdRows) {
+        g = blockIdx.x % kXcdGroups;   // round-robin block -> XCD deal: group g stays in one XCD's L2
+        q0 = blockIdx.x / kXcdGroups;
+        step = gridDim.x / kXcdGroups;
+        nt = (src.pstart[g + 1] - src.pstart[g] + kXcdTileBuckets - 1) / kXcdTileBuckets;
+    } else {
+        g = 0;
+        q0 = blockIdx.x;
+        step = gridDim.x;
+        nt = (unsigned long long)((src.n + kProbeTile - 1) / kProbeTile);
+    }
+}
+
 // ------------------------------------------------------------------ probe
 // count (join_v1.mlir:288-425, join_v2.mlir:311-439) and probe
 // (join_v1.mlir:436-521, join_v2.mlir:450-604) in one kernel family.
@@ -190,7 +240,6 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
     using LY = Lay<L>;
     using slot_t = typename LY::slot_t;
     using out_t = typename LY::out_t;
-    constexpr int kTile = kBlock * kProbeItems;
     constexpr int NW = kBlock / 64;
     __shared__ unsigned long long st_base;
     __shared__ unsigned long long wsum[NW];
@@ -198,97 +247,100 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
 
     const slot_t *sl = (const slot_t *)t.slots;
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
-
-    const long long base = (long long)blockIdx.x * kTile + threadIdx.x;
-    unsigned long long K[kProbeItems], P[kProbeItems];
-    bool V[kProbeItems];
-    bool has_null = false;
-#pragma unroll
-    for (int i = 0; i < kProbeItems; ++i) {
-        const long long row = base + (long long)i * kBlock;
-        V[i] = row < src.n;
-        Tuple tp = V[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
-        K[i] = tp.k;
-        P[i] = tp.p;
-        has_null |= V[i] && LY::null_key(K[i]);
-    }
-    if (!unique || __syncthreads_or(has_null ? 1 : 0)) {
-        // general path: k_probe_slow takes this tile
-        if (threadIdx.x == 0) slow[atomicAdd(&t.meta[3], 1ull)] = blockIdx.x;
-        return;
-    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    slot_t S[kProbeItems];
-    unsigned long long H[kProbeItems];
-#pragma unroll
-    for (int i = 0; i < kProbeItems; ++i) {
-        H[i] = slot_of(K[i], t.shift);
-        if (V[i]) S[i] = sl[H[i]];
-    }
-    unsigned found = 0;
-    unsigned long long RP[kProbeItems];
-#pragma unroll
-    for (int i = 0; i < kProbeItems; ++i) {
-        RP[i] = 0;
-        if (!V[i]) continue;
-        slot_t sv = S[i];
-        unsigned long long hh = H[i];
-        while (!LY::empty(sv)) {
-            if (LY::key(sv) == K[i]) {
-                found |= 1u << i;
-                RP[i] = LY::pay(sv);
-                break;
-            }
-            hh = (hh + 1) & t.mask;
-            sv = sl[hh];
-        }
-    }
-    if constexpr (!WRITE) {
-        unsigned long long c = (unsigned long long)__popc(found);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
-        if (lane == 0) wsum[wv] = c;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tot = 0;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) tot += wsum[w];
-            if (tot) atomicAdd(out.counter, tot);
-        }
-    } else {
-        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        unsigned lpre[kProbeItems];
+    unsigned g;
+    unsigned long long q0, step, nt;
+    probe_tiles<FORM>(src, g, q0, step, nt);
+    for (unsigned long long q = q0; q < nt; q += step) {
+        unsigned long long K[kProbeItems], P[kProbeItems];
+        bool V[kProbeItems];
+        bool has_null = false;
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
-            const unsigned long long bal = __ballot((found >> i) & 1u);
-            lpre[i] = (unsigned)__popcll(bal & lt);
-            if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+            Tuple tp{0ull, 0ull};
+            V[i] = probe_row<L, FORM>(src, g, q, i, tp);
+            K[i] = tp.k;
+            P[i] = tp.p;
+            has_null |= V[i] && LY::null_key(K[i]);
         }
-        __syncthreads();
-        if (wv == 0) {   // exclusive scan of the kProbeItems * NW runs (<= 64)
-            static_assert(kProbeItems * NW <= 64, "one lane per run");
-            const unsigned v = lane < kProbeItems * NW ? s_cw[lane] : 0u;
-            unsigned x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (lane < kProbeItems * NW) s_cw[lane] = x - v;
-            if (lane == 63) st_base = x ? atomicAdd(out.counter, (unsigned long long)x) : 0ull;
+        if (!unique || __syncthreads_or(has_null ? 1 : 0)) {
+            // general path: k_probe_slow takes this tile
+            if (threadIdx.x == 0) slow[atomicAdd(&t.meta[3], 1ull)] = (unsigned)(q * kXcdGroups + g);
+            continue;
         }
-        __syncthreads();
-        out_t *orr = (out_t *)out.r;
-        out_t *oss = (out_t *)out.s;
+        slot_t S[kProbeItems];
+        unsigned long long H[kProbeItems];
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
-            if (!((found >> i) & 1u)) continue;
-            const unsigned long long g = st_base + s_cw[i * NW + wv] + lpre[i];
-            if (g < (unsigned long long)out.cap) {
-                orr[g] = (out_t)RP[i];
-                oss[g] = (out_t)P[i];
+            H[i] = slot_of(K[i], t.shift);
+            if (V[i]) S[i] = sl[H[i]];
+        }
+        unsigned found = 0;
+        unsigned long long RP[kProbeItems];
+#pragma unroll
+        for (int i = 0; i < kProbeItems; ++i) {
+            RP[i] = 0;
+            if (!V[i]) continue;
+            slot_t sv = S[i];
+            unsigned long long hh = H[i];
+            while (!LY::empty(sv)) {
+                if (LY::key(sv) == K[i]) {
+                    found |= 1u << i;
+                    RP[i] = LY::pay(sv);
+                    break;
+                }
+                hh = (hh + 1) & t.mask;
+                sv = sl[hh];
             }
         }
+        if constexpr (!WRITE) {
+            unsigned long long c = (unsigned long long)__popc(found);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+            if (lane == 0) wsum[wv] = c;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long tot = 0;
+#pragma unroll
+                for (int w = 0; w < NW; ++w) tot += wsum[w];
+                if (tot) atomicAdd(out.counter, tot);
+            }
+        } else {
+            const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            unsigned lpre[kProbeItems];
+#pragma unroll
+            for (int i = 0; i < kProbeItems; ++i) {
+                const unsigned long long bal = __ballot((found >> i) & 1u);
+                lpre[i] = (unsigned)__popcll(bal & lt);
+                if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+            }
+            __syncthreads();
+            if (wv == 0) {   // exclusive scan of the kProbeItems * NW runs (<= 64)
+                static_assert(kProbeItems * NW <= 64, "one lane per run");
+                const unsigned v = lane < kProbeItems * NW ? s_cw[lane] : 0u;
+                unsigned x = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const unsigned y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                if (lane < kProbeItems * NW) s_cw[lane] = x - v;
+                if (lane == 63) st_base = x ? atomicAdd(out.counter, (unsigned long long)x) : 0ull;
+            }
+            __syncthreads();
+            out_t *orr = (out_t *)out.r;
+            out_t *oss = (out_t *)out.s;
+#pragma unroll
+            for (int i = 0; i < kProbeItems; ++i) {
+                if (!((found >> i) & 1u)) continue;
+                const unsigned long long gi = st_base + s_cw[i * NW + wv] + lpre[i];
+                if (gi < (unsigned long long)out.cap) {
+                    orr[gi] = (out_t)RP[i];
+                    oss[gi] = (out_t)P[i];
+                }
+            }
+        }
+        __syncthreads();   // s_cw / st_base / wsum reused by the next tile
     }
 }
 
@@ -299,7 +351,6 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
     using LY = Lay<L>;
     using slot_t = typename LY::slot_t;
     using out_t = typename LY::out_t;
-    constexpr int kTile = kBlock * kProbeItems;
     constexpr int kStage = 1024;
     constexpr int NW = kBlock / 64;
     __shared__ out_t st_r[WRITE ? kStage : 1];
@@ -313,14 +364,13 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
     const unsigned long long ntiles = t.meta[3];
     for (unsigned long long j = blockIdx.x; j < ntiles; j += gridDim.x) {
         if (threadIdx.x == 0) st_n = 0u;
-        const long long base = (long long)slow[j] * kTile + threadIdx.x;
+        const unsigned id = slow[j];
         unsigned long long K[kProbeItems], P[kProbeItems];
         bool V[kProbeItems];
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
-            const long long row = base + (long long)i * kBlock;
-            V[i] = row < src.n;
-            Tuple tp = V[i] ? load_src<FORM>(src, row) : Tuple{0ull, 0ull};
+            Tuple tp{0ull, 0ull};
+            V[i] = probe_row<L, FORM>(src, id % kXcdGroups, id / kXcdGroups, i, tp);
             K[i] = tp.k;
             P[i] = tp.p;
         }
@@ -716,17 +766,24 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
     return hipGetLastError();
 }
 
-size_t probe_tiles(long long n) { return (size_t)(n > 0 ? (n + kBlock * kProbeItems - 1) / (kBlock * kProbeItems) : 0); }
+size_t probe_tiles(long long n) {
+    // plain tiles, or XCD-group tiles: a group's buckets are <= n / 512 full
+    // ones plus <= (256 workgroups + 2) x 8 open ones, 4 buckets per tile,
+    // one partial tile per group
+    return (size_t)(n > 0 ? (n + kProbeTile - 1) / kProbeTile : 0) + 1024;
+}
 
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
                         bool count_only, unsigned *slow, hipStream_t st) {
     if (src.n <= 0) return hipSuccess;
-    const unsigned g = grid_for(src.n, kBlock * kProbeItems);
     hipError_t e = hipMemsetAsync(&t.meta[3], 0, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned gs = g < (unsigned)(cus * 8) ? g : (unsigned)(cus * 8);
+    const unsigned tiles = grid_for(src.n, kProbeTile);
+    // plain: one block per tile; XCD groups: a persistent grid, a multiple of 8
+    const unsigned g = src.form == kXcdRows ? (unsigned)(cus * 4) / kXcdGroups * kXcdGroups : tiles;
+    const unsigned gs = tiles < (unsigned)(cus * 8) ? tiles : (unsigned)(cus * 8);
 #define HJ_PROBE(L, F)                                                                                        \
     do {                                                                                                      \
         if (count_only) {                                                                                     \
@@ -742,9 +799,11 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
     if (layout == kWide) {
         if (src.form == kCols64) HJ_PROBE(kWide, kCols64);
         else if (src.form == kPacked64) HJ_PROBE(kWide, kPacked64);
+        else if (src.form == kXcdRows) HJ_PROBE(kWide, kXcdRows);
         else return hipErrorInvalidValue;
     } else {
         if (src.form == kCol32) HJ_PROBE(kNarrow, kCol32);
+        else if (src.form == kXcdRows) HJ_PROBE(kNarrow, kXcdRows);
         else return hipErrorInvalidValue;
     }
 #undef HJ_PROBE

@@ -320,3 +320,44 @@ def test_i32_reference_scale(hj):
     assert m == _independent_count(r.long(), s.long())
     assert bool((r[o_r.long()] == s[o_s.long()]).all())
     assert torch.unique(o_r.long() * n + o_s.long()).numel() == m
+
+
+# ---------------------------------------------------------------- XCD split
+# Global-table probe with the probe side routed into 8 groups by the top slot
+# bits (one group per XCD).  Forced on at oracle-checkable sizes; the fast
+# path, the general path (duplicates, INT64_MIN keys) on bucketed tiles and
+# the i32 layout must all match the oracle.
+@pytest.mark.parametrize("case", ["pkfk", "dups", "nulls", "i32"])
+def test_xcd_split_vs_oracle(oracle, case):
+    hj = HashJoin(0)
+    try:
+        hj.set_strategy("global")
+        hj.set_xcd_split(True)
+        hj.set_timing(True)
+        if case == "pkfk":
+            rk, rp, sk, sp = oracle.gen_pkfk_i64(5, 100000, 300000, 0.7)
+            exp = oracle.chained_join_i64(rk, rp, sk, sp, H=1000)
+        elif case == "dups":
+            rk, rp = oracle.gen_uniform_i64(6, 1, 1, 5000, 40000)
+            sk, sp = oracle.gen_uniform_i64(6, 2, 1, 5000, 90000)
+            exp = oracle.chained_join_i64(rk, rp, sk, sp, H=500)
+        elif case == "nulls":
+            rk, rp = oracle.gen_uniform_i64(7, 1, -200, 200, 20000)
+            sk, sp = oracle.gen_uniform_i64(7, 2, -200, 200, 30000)
+            rk[::101] = -(1 << 63); sk[::103] = -(1 << 63)
+            exp = oracle.nested_loop_i64(rk, rp, sk, sp)
+        else:
+            r = oracle.gen_uniform_i32(8, 1, 1, 1 << 20, 50000)
+            s = oracle.gen_uniform_i32(8, 2, 1, 1 << 20, 120000)
+            o_r, o_s = hj.join(torch.from_numpy(r).cuda(), None, torch.from_numpy(s).cuda(), None)
+            assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
+                                        *oracle.chained_join_i32(r, s, H=1000))
+            return
+        d = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (rk, rp, sk, sp)]
+        o_r, o_s = hj.join(*d)
+        assert hj.strategy_used == "global"
+        assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp)
+        t = hj.last_timing()
+        assert t["probe_partition"] > 0          # the split ran
+    finally:
+        hj.close()
