@@ -781,8 +781,9 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned tiles = grid_for(src.n, kProbeTile);
-    // plain: one block per tile; XCD groups: a persistent grid, a multiple of 8
-    const unsigned g = src.form == kXcdRows ? (unsigned)(cus * 4) / kXcdGroups * kXcdGroups : tiles;
+    // plain: one block per tile; XCD groups: a strided grid, a multiple of 8,
+    // 20 workgroups per CU (C2 sweep 4/5/10/20: 20 is fastest)
+    const unsigned g = src.form == kXcdRows ? (unsigned)(cus * 20) / kXcdGroups * kXcdGroups : tiles;
     const unsigned gs = tiles < (unsigned)(cus * 8) ? tiles : (unsigned)(cus * 8);
 #define HJ_PROBE(L, F)                                                                                        \
     do {                                                                                                      \
