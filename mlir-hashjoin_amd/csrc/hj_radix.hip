@@ -42,7 +42,7 @@ namespace {
 
 typedef unsigned long long u64;
 constexpr u64 kGold = 0x9E3779B97F4A7C15ull;
-constexpr int kTile = 8192;        // rows per partition-pass tile (LDS staging: 128 KiB wide)
+constexpr int kTile = 4096;        // rows per partition-pass tile (LDS staging: 64 KiB wide)
 constexpr int kPassThreads = 1024; // one workgroup per CU
 constexpr int kPassRows = kTile / kPassThreads;
 constexpr int kMaxFan = 512;       // bins per pass (9 bits)
@@ -269,15 +269,24 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, u
 // [w*T/G, (w+1)*T/G); its open bucket per bin lives in LDS (cur, fill) and
 // is closed (bfill written) when the workgroup moves to another segment or
 // finishes, so at most (G + nseg) * F buckets are ever partly filled.
-// ABL (diagnostics only, micro/pass_micro.hip; the product uses 0): 1 no row
-// stores, 2 synthetic rows instead of loads, 4 rows stored back in tile order
-// (contiguous) instead of to their buckets, 8 runs start on 128-B lines.
-template <bool WIDE, int FORM, int ABL = 0>
+//
+// Only whole 128-B lines are written.  A bin's run from one tile starts and
+// ends inside lines, and a line stored in two parts costs the HBM a
+// read-modify-write: 2.47 ms per 2^28-row pass with unaligned 256-B runs
+// against 1.67 ms for the same traffic in aligned runs
+// (profiles/r01_micro_write_alignment.txt, micro/ws_micro.hip).  So each bin
+// keeps the rows of its last, incomplete line in LDS (tail, < L rows) and
+// writes them with the line's remaining rows from a later tile; a bucket
+// holds a whole number of lines, and only the final line of a workgroup's
+// open bucket is ever written partly (at close).
+template <bool WIDE, int FORM>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     constexpr int IT = kPassRows;
+    constexpr unsigned L = 128 / sizeof(T);   // rows per line
     __shared__ T stage[kTile];
+    __shared__ T tail[kMaxFan * (L - 1)];   // bin b: rows of positions [fill & ~(L-1), fill)
     __shared__ unsigned short sb[kTile];
     __shared__ unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan], nbase[kMaxFan];
     __shared__ unsigned s_nb;   // first fresh bucket of the current tile
@@ -290,32 +299,31 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
         cnt[b] = 0u;
         cur[b] = kNoBucket;
-        fill[b] = PB;
+        fill[b] = PB;   // no open bucket (and no tail: PB is a whole number of lines)
     }
-    // ABL 8 (diagnostic): every run starts on a 128-B line (wastes space)
-    auto afill = [&](unsigned f) -> unsigned {
-        if constexpr ((ABL & 8) != 0) return f >= PB ? f : ((f + 7u) & ~7u) > PB ? PB : ((f + 7u) & ~7u);
-        return f;
+    // row slot of position p (>= the line start of fill[b]) of bin b's run
+    // in the current tile: the open bucket, then the tile's fresh buckets
+    auto slot = [&](unsigned b, unsigned p) -> u64 {
+        const unsigned k = p >> a.out_pbl;
+        const unsigned bk = k == 0 ? cur[b] : (s_nb == kNoBucket ? kNoBucket : s_nb + nbase[b] + k - 1);
+        return bk < a.max_buckets ? ((u64)bk << a.out_pbl) + (p & (PB - 1)) : ~0ull;
     };
     int seg_cur = -1;
-    // close this workgroup's open buckets (their fill is final)
+    // close this workgroup's open buckets: write each tail (the bucket's
+    // last, partial line); their fill is final
     auto close_all = [&]() {
         for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
-            if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = fill[b];
+            const unsigned f = fill[b], tl = f & (L - 1);
+            if (cur[b] != kNoBucket && cur[b] < a.max_buckets) {
+                for (unsigned i = 0; i < tl; ++i) out[((u64)cur[b] << a.out_pbl) + (f - tl + i)] = tail[b * (L - 1) + i];
+                a.bfill[cur[b]] = f;
+            }
             cur[b] = kNoBucket;
             fill[b] = PB;
         }
     };
-    for (unsigned t = t0; t < t1; ++t) {
-        const PassTile tl = pass_tile<FORM>(a, t);
-        if (tl.seg != seg_cur) {   // uniform: every thread sees the same tile
-            __syncthreads();
-            close_all();
-            seg_cur = tl.seg;
-            __syncthreads();
-        }
-        T row[IT];
-        unsigned br[IT];   // bin << 16 | rank within the tile's bin
+    // rows of tile tl into registers (br = 0 valid, ~0 none)
+    auto load_tile = [&](const PassTile &tl, T (&row)[IT], unsigned (&br)[IT]) {
         if constexpr (WIDE && FORM == kCols64) {
             // two consecutive rows per lane: one 16-B load from each column
             // (rows lo + 2 * (i * NT + t) + {0, 1}; order inside a tile is free)
@@ -340,12 +348,6 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         } else {
 #pragma unroll
             for (int i = 0; i < IT; ++i) {
-                if constexpr ((ABL & 2) != 0) {
-                    const u64 v = (u64)t * kTile + (u64)i * kPassThreads + threadIdx.x;
-                    row[i] = R::make(fmix64(v), v);
-                    br[i] = 0u;
-                    continue;
-                }
                 if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
                     row[i] = R::zero();
                     br[i] = 0xFFFFFFFFu;
@@ -353,6 +355,21 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                     br[i] = 0u;
                 }
             }
+        }
+    };
+    T row[IT];
+    unsigned br[IT];   // bin << 16 | rank within the tile's bin
+    PassTile tl{};
+    if (t0 < t1) {
+        tl = pass_tile<FORM>(a, t0);
+        load_tile(tl, row, br);
+    }
+    for (unsigned t = t0; t < t1; ++t) {
+        if (tl.seg != seg_cur) {   // uniform: every thread sees the same tile
+            __syncthreads();
+            close_all();
+            seg_cur = tl.seg;
+            __syncthreads();
         }
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
@@ -372,7 +389,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             for (int j = 0; j < 8; ++j) {
                 const unsigned b = lane * 8 + j;
                 c[j] = b < F ? cnt[b] : 0u;
-                k[j] = c[j] ? (afill(fill[b]) + c[j] - 1) >> a.out_pbl : 0u;
+                k[j] = c[j] ? (fill[b] + c[j] - 1) >> a.out_pbl : 0u;
                 s += c[j];
                 sk += k[j];
             }
@@ -412,35 +429,58 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             sb[pos] = (unsigned short)b;
         }
         __syncthreads();
+        // the next tile's loads are in flight during this tile's stores
+        const int seg = tl.seg;
+        if (t + 1 < t1) {
+            tl = pass_tile<FORM>(a, t + 1);
+            load_tile(tl, row, br);
+        }
+        // Bin b's rows now span positions [fill, fill + cnt) of its bucket
+        // run; lines end below E = (fill + cnt) & ~(L - 1).  Rows below E
+        // are stored (the tail's first), the rest become the new tail.
         const unsigned tn = start[F - 1] + cnt[F - 1];
+        unsigned tpos[IT];   // new tail index of staged row j, or ~0
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
             const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
+            tpos[i] = 0xFFFFFFFFu;
             if (j >= tn) continue;
             const unsigned b = sb[j];
-            const unsigned p = afill(fill[b]) + (j - start[b]);
-            const unsigned k = p >> a.out_pbl;
-            const unsigned bk = k == 0 ? cur[b] : (s_nb == kNoBucket ? kNoBucket : s_nb + nbase[b] + k - 1);
-            if constexpr ((ABL & 1) != 0) continue;
-            if constexpr ((ABL & 4) != 0) {
-                out[(u64)t * kTile + j] = stage[j];
+            const unsigned f = fill[b];
+            const unsigned p = f + (j - start[b]), e = (f + cnt[b]) & ~(L - 1);
+            if (p >= e) {
+                tpos[i] = b * (L - 1) + (p - e);
                 continue;
             }
-            if (bk < a.max_buckets) out[((u64)bk << a.out_pbl) + (p & (PB - 1))] = stage[j];
+            const u64 o = slot(b, p);
+            if (o != ~0ull) out[o] = stage[j];
+        }
+        for (unsigned q = threadIdx.x; q < F * (L - 1); q += kPassThreads) {
+            const unsigned b = q / (L - 1), i = q - b * (L - 1);
+            const unsigned f = fill[b], tl0 = f & (L - 1);
+            if (i >= tl0) continue;
+            const unsigned p = f - tl0 + i;
+            if (p >= ((f + cnt[b]) & ~(L - 1))) continue;   // line still incomplete: stays
+            const u64 o = slot(b, p);
+            if (o != ~0ull) out[o] = tail[q];
         }
         __syncthreads();
+#pragma unroll
+        for (int i = 0; i < IT; ++i)
+            if (tpos[i] != 0xFFFFFFFFu) tail[tpos[i]] = stage[(unsigned)i * kPassThreads + threadIdx.x];
         for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
             const unsigned c = cnt[b];
             cnt[b] = 0u;
             if (!c) continue;
-            const unsigned f = afill(fill[b]);
+            const unsigned f = fill[b];
             const unsigned k = (f + c - 1) >> a.out_pbl;
             if (k) {
-                // the replaced open bucket is full; record the fresh ones
+                // the replaced open bucket is full (all its lines stored);
+                // record the fresh ones
                 if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
                 if (s_nb != kNoBucket) {
                     const unsigned nb = s_nb + nbase[b];
-                    const unsigned pid = ((unsigned)tl.seg << a.fbits) | b;
+                    const unsigned pid = ((unsigned)seg << a.fbits) | b;
                     for (unsigned i = 0; i < k; ++i) {
                         a.bbin[nb + i] = pid;
                         if (i + 1 < k) a.bfill[nb + i] = PB;

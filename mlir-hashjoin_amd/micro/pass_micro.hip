@@ -1,7 +1,8 @@
 // pass_micro.hip -- ablation of the partition pass kernel (k_pass) on 2^28
 // packed 16-B rows, first pass (512 bins) and a 256-bin pass.
-// ABL bits: 1 no row stores, 2 synthetic rows instead of loads, 4 rows stored
-// contiguously (tile order) instead of to their buckets.
+// (The ablation of the earlier kernel is kept in
+// profiles/r01_micro_pass_ablation.txt; micro/ws_micro.hip isolates the
+// write pattern.)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../csrc -I../../include -o pass_micro pass_micro.hip
 #include "../csrc/hj_radix.hip"
 
@@ -66,16 +67,8 @@ int main() {
         for (int pbl : {9, 8}) {
             a.out_pbl = pbl;
             char nm[64];
-#define P(ABL, TXT)                                                                                     \
-    snprintf(nm, sizeof nm, "F%d PB%d %s", 1 << fb, 1 << pbl, TXT);                                     \
-    run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a); })
-            P(0, "full");
-            P(1, "no stores");
-            P(2, "synthetic rows");
-            P(3, "no loads, no stores (LDS only)");
-            P(4, "contiguous stores");
-            P(8, "line-aligned runs");
-#undef P
+            snprintf(nm, sizeof nm, "F%d PB%d k_pass", 1 << fb, 1 << pbl);
+            run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow>), dim3(grid), dim3(kPassThreads), 0, 0, a); });
         }
     }
     return 0;
