@@ -505,9 +505,12 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
 constexpr int kListPer = 4;
 constexpr int kListLds = 4096;
 
-__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *nb, u64 *pcnt, int P) {
+// Buckets [0, *nb) of a pass, clamped to the set's capacity (the counter
+// passes it only when a pass ran out of buckets, which radix_need excludes).
+__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *nb, unsigned max_buckets,
+                                                 u64 *pcnt, int P) {
     __shared__ unsigned c[kListLds];
-    const unsigned n = *nb;
+    const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
     const bool lds = P <= kListLds;
@@ -529,10 +532,10 @@ __global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const uns
 }
 
 __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 u64 *pcur, u64 *blist, int P) {
+                                                 unsigned max_buckets, u64 *pcur, u64 *blist, int P) {
     __shared__ unsigned c[kListLds];
     __shared__ u64 cb[kListLds];
-    const unsigned n = *nb;
+    const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
     if (P > kListLds) {
@@ -1127,12 +1130,13 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         if (e != hipSuccess) return e;
         const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
         hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin, (const unsigned *)ws.nb,
-                           dst.pstart, (int)P);
+                           a.max_buckets, dst.pstart, (int)P);
         scan_u64(dst.pstart, P + 1, ws.scan_sums, st);
         e = hipMemcpyAsync(ws.pcur, dst.pstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, ws.pcur, dst.blist, (int)P);
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, ws.pcur, dst.blist,
+                           (int)P);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         prev = &dst;
