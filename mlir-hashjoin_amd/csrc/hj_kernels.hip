@@ -466,16 +466,50 @@ __device__ __forceinline__ unsigned part_of(unsigned long long k, unsigned P) {
     return (unsigned)(((fmix64(k) >> 32) * (unsigned long long)P) >> 32);
 }
 
+// Parts at most this many: LDS counter updates are aggregated per wave (one
+// atomic per distinct part and wave instead of one per lane: with 1-8 parts
+// every lane of a wave hits the same few counters).
+constexpr unsigned kAggParts = 16;
+
+// Wave-aggregated cnt[d] += 1 for every lane with `valid`; returns the lane's
+// rank among the lanes of its wave and part, offset by the counter's old
+// value.  All 64 lanes must call it (ballots).
+__device__ __forceinline__ unsigned agg_add(unsigned *cnt, unsigned d, bool valid) {
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    unsigned long long todo = __ballot(valid);
+    unsigned rank = 0u;
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const unsigned dl = __shfl(d, leader, 64);
+        const bool mine = valid && d == dl;
+        const unsigned long long m = __ballot(mine);
+        unsigned b = 0u;
+        if ((int)lane == leader) b = atomicAdd(&cnt[dl], (unsigned)__popcll(m));
+        b = __shfl(b, leader, 64);
+        if (mine) rank = b + (unsigned)__popcll(m & lt);
+        todo &= ~m;
+    }
+    return rank;
+}
+
 template <int FORM>
 __global__ __launch_bounds__(kBlock) void k_part_hist(SrcDev src, unsigned P, unsigned long long *counts) {
     extern __shared__ unsigned lds_hist[];
     for (unsigned i = threadIdx.x; i < P; i += kBlock) lds_hist[i] = 0u;
     __syncthreads();
-    const long long base = (long long)blockIdx.x * (kBlock * kPartItems) + threadIdx.x;
+    // grid-stride over 2048-row chunks: one flush of the block's counts at
+    // the end (a flush per chunk put ~10^5 atomics on each part's counter)
+    for (long long base = (long long)blockIdx.x * (kBlock * kPartItems) + threadIdx.x; base - threadIdx.x < src.n;
+         base += (long long)gridDim.x * (kBlock * kPartItems)) {
 #pragma unroll
-    for (int i = 0; i < kPartItems; ++i) {
-        const long long row = base + (long long)i * kBlock;
-        if (row < src.n) atomicAdd(&lds_hist[part_of(load_src<FORM>(src, row).k, P)], 1u);
+        for (int i = 0; i < kPartItems; ++i) {
+            const long long row = base + (long long)i * kBlock;
+            const bool v = row < src.n;
+            const unsigned d = v ? part_of(load_src<FORM>(src, row).k, P) : 0u;
+            if (P <= kAggParts) (void)agg_add(lds_hist, d, v);
+            else if (v) atomicAdd(&lds_hist[d], 1u);
+        }
     }
     __syncthreads();
     for (unsigned i = threadIdx.x; i < P; i += kBlock)
@@ -529,6 +563,118 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P,
         if (pid[i] == ~0u) continue;
         const unsigned r = atomicAdd(&cnt[pid[i]], 1u);
         out[bases[pid[i]] + r] = make_ulonglong2(k[i], p[i]);
+    }
+}
+
+// Staged scatter for up to kRouteMaxParts parts: one 8192-row tile per
+// workgroup is counting-sorted by part in LDS and every part's run is then
+// written by consecutive lanes to consecutive addresses.  k_part_scatter
+// writes each row to its own rank slot (lanes of a wave hit unrelated
+// addresses and most 128-B lines are written in pieces, each a
+// read-modify-write in HBM: profiles/r01_micro_write_alignment.txt).
+constexpr int kRouteTile = 8192;
+constexpr int kRouteThreads = 1024;
+constexpr int kRouteMaxParts = 512;
+
+template <int FORM>
+__global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, unsigned P, ulonglong2 *out,
+                                                                 unsigned long long *cursors) {
+    constexpr int IT = kRouteTile / kRouteThreads;
+    __shared__ ulonglong2 stage[kRouteTile];
+    __shared__ unsigned short sp[kRouteTile];
+    __shared__ unsigned cnt[kRouteMaxParts], start[kRouteMaxParts];
+    __shared__ unsigned long long base[kRouteMaxParts];
+    for (unsigned i = threadIdx.x; i < P; i += kRouteThreads) cnt[i] = 0u;
+    __syncthreads();
+    const long long lo = (long long)blockIdx.x * kRouteTile;
+    ulonglong2 row[IT];
+    unsigned pr[IT];   // part << 16 | rank, or ~0
+    if constexpr (FORM == kCols64) {
+        // two consecutive rows per lane: one 16-B load from each column
+        const unsigned long long *kc = (const unsigned long long *)src.key, *pc = (const unsigned long long *)src.pay;
+        const bool al = ((((uintptr_t)kc) | ((uintptr_t)pc)) & 15) == 0;
+#pragma unroll
+        for (int i = 0; i < IT / 2; ++i) {
+            const long long r = lo + 2ll * (i * kRouteThreads + threadIdx.x);
+            if (al && r + 1 < src.n) {
+                const ulonglong2 k2 = *(const ulonglong2 *)(kc + r), p2 = *(const ulonglong2 *)(pc + r);
+                row[2 * i] = make_ulonglong2(k2.x, p2.x);
+                row[2 * i + 1] = make_ulonglong2(k2.y, p2.y);
+                pr[2 * i] = pr[2 * i + 1] = 0u;
+            } else {
+                const bool v0 = r < src.n, v1 = r + 1 < src.n;
+                row[2 * i] = v0 ? make_ulonglong2(kc[r], pc[r]) : make_ulonglong2(0ull, 0ull);
+                row[2 * i + 1] = v1 ? make_ulonglong2(kc[r + 1], pc[r + 1]) : make_ulonglong2(0ull, 0ull);
+                pr[2 * i] = v0 ? 0u : ~0u;
+                pr[2 * i + 1] = v1 ? 0u : ~0u;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const long long r = lo + (long long)i * kRouteThreads + threadIdx.x;
+            const bool v = r < src.n;
+            const Tuple tp = v ? load_src<FORM>(src, r) : Tuple{0ull, 0ull};
+            row[i] = make_ulonglong2(tp.k, tp.p);
+            pr[i] = v ? 0u : ~0u;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const bool v = pr[i] != ~0u;
+        const unsigned d = v ? part_of(row[i].x, P) : 0u;
+        if (P <= kAggParts) {
+            const unsigned r = agg_add(cnt, d, v);
+            if (v) pr[i] = (d << 16) | r;
+        } else if (v) {
+            pr[i] = (d << 16) | atomicAdd(&cnt[d], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {   // wave 0: stage offsets; one cursor atomic per non-empty part
+        const unsigned lane = threadIdx.x;
+        constexpr int PER = kRouteMaxParts / 64;
+        unsigned c[PER], sum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const unsigned d = lane * PER + j;
+            c[j] = d < P ? cnt[d] : 0u;
+            sum += c[j];
+        }
+        unsigned x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        unsigned run = x - sum;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const unsigned d = lane * PER + j;
+            if (d < P) {
+                start[d] = run;
+                base[d] = c[j] ? atomicAdd(&cursors[d], (unsigned long long)c[j]) : 0ull;
+            }
+            run += c[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        if (pr[i] == ~0u) continue;
+        const unsigned d = pr[i] >> 16, pos = start[d] + (pr[i] & 0xffffu);
+        stage[pos] = row[i];
+        sp[pos] = (unsigned short)d;
+    }
+    __syncthreads();
+    const long long rem = src.n - lo;
+    const unsigned tn = rem < kRouteTile ? (unsigned)rem : (unsigned)kRouteTile;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const unsigned j = (unsigned)i * kRouteThreads + threadIdx.x;
+        if (j >= tn) continue;
+        const unsigned d = sp[j];
+        out[base[d] + (j - start[d])] = stage[j];
     }
 }
 
@@ -818,13 +964,24 @@ hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
     if (e != hipSuccess) return e;
     if (src.n > 0) {
         const unsigned g = grid_for(src.n, kBlock * kPartItems);
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const unsigned gh = g < (unsigned)cus * 8u ? g : (unsigned)cus * 8u;
         const size_t lds_h = sizeof(unsigned) * P;
         const size_t lds_s = sizeof(unsigned) * ((P + 1) & ~1u) + sizeof(unsigned long long) * P;
-        if (src.form == kCols64) hipLaunchKernelGGL(k_part_hist<kCols64>, dim3(g), dim3(kBlock), lds_h, st, src, P, counts);
-        else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(g), dim3(kBlock), lds_h, st, src, P, counts);
+        if (src.form == kCols64) hipLaunchKernelGGL(k_part_hist<kCols64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, counts);
+        else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, counts);
         else return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(64), 0, st, counts, P, cursors);
-        if (src.form == kCols64)
+        if (P <= (unsigned)kRouteMaxParts) {
+            const unsigned gt = grid_for(src.n, kRouteTile);
+            if (src.form == kCols64)
+                hipLaunchKernelGGL(k_route_scatter<kCols64>, dim3(gt), dim3(kRouteThreads), 0, st, src, P,
+                                   (ulonglong2 *)out_tuples, cursors);
+            else
+                hipLaunchKernelGGL(k_route_scatter<kPacked64>, dim3(gt), dim3(kRouteThreads), 0, st, src, P,
+                                   (ulonglong2 *)out_tuples, cursors);
+        } else if (src.form == kCols64)
             hipLaunchKernelGGL(k_part_scatter<kCols64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
         else
             hipLaunchKernelGGL(k_part_scatter<kPacked64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
