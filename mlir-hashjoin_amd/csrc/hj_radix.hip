@@ -610,7 +610,8 @@ __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, c
 // sub-chunks of NT * SI / PB buckets.  Requires PB | RCAP
 // and PB | NT * SI (host-checked).
 // ABL (diagnostics only, micro/join_micro.hip; the product uses 0) switches
-// phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build.
+// phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build,
+// 16 probe reads the first slot only.
 template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems>
 __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per SIMD: <= 128 VGPRs
     typedef Row<WIDE> R;
@@ -792,6 +793,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                                 break;
                             }
                         }
+                        if constexpr ((ABL & 16) != 0) break;
                         h = (h + 1) & kMask;
                         e = tkey[h];
                     }

@@ -142,6 +142,8 @@ int main() {
     J(12, 512, 2, true, 1, "no atomic");
     J(12, 512, 2, true, 2, "no writes");
     J(12, 512, 2, true, 3, "no atomic, no writes");
+    J(12, 512, 2, true, 19, "no atomic/writes, 1st-slot probe");
+    J(12, 512, 2, true, 11, "no atomic/writes/build");
     J(12, 512, 2, true, 7, "no probe/atomic/writes");
     J(12, 512, 2, true, 15, "loads + init only");
     return 0;
