@@ -279,7 +279,10 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, u
 // writes them with the line's remaining rows from a later tile; a bucket
 // holds a whole number of lines, and only the final line of a workgroup's
 // open bucket is ever written partly (at close).
-template <bool WIDE, int FORM>
+// ABL (diagnostics only, micro/pass_micro.hip; the product uses 0): 1 fresh
+// buckets from a fixed per-tile range instead of the global atomic, 2
+// synthetic rows instead of loads, 4 no row stores (rows and tails).
+template <bool WIDE, int FORM, int ABL = 0>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -324,7 +327,14 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     };
     // rows of tile tl into registers (br = 0 valid, ~0 none)
     auto load_tile = [&](const PassTile &tl, T (&row)[IT], unsigned (&br)[IT]) {
-        if constexpr (WIDE && FORM == kCols64) {
+        if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int i = 0; i < IT; ++i) {
+                const u64 v = tl.lo * 7 + (u64)i * kPassThreads + threadIdx.x;
+                row[i] = R::make(fmix64(v), v);
+                br[i] = 0u;
+            }
+        } else if constexpr (WIDE && FORM == kCols64) {
             // two consecutive rows per lane: one 16-B load from each column
             // (rows lo + 2 * (i * NT + t) + {0, 1}; order inside a tile is free)
             const u64 *kc = (const u64 *)a.in.key, *pc = (const u64 *)a.in.pay;
@@ -414,7 +424,8 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 runk += k[j];
             }
             if (lane == 63) {
-                unsigned nb = xk ? atomicAdd(a.nb, xk) : 0u;
+                unsigned nb = (ABL & 1) ? (unsigned)(((u64)tl.lo / kTile * 24u) % (a.max_buckets - 1024u))
+                                        : (xk ? atomicAdd(a.nb, xk) : 0u);
                 if ((u64)nb + xk > a.max_buckets) nb = kNoBucket;   // cannot happen within radix_need
                 s_nb = nb;
             }
@@ -453,7 +464,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 continue;
             }
             const u64 o = slot(b, p);
-            if (o != ~0ull) out[o] = stage[j];
+            if ((ABL & 4) == 0 && o != ~0ull) out[o] = stage[j];
         }
         for (unsigned q = threadIdx.x; q < F * (L - 1); q += kPassThreads) {
             const unsigned b = q / (L - 1), i = q - b * (L - 1);
@@ -462,7 +473,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const unsigned p = f - tl0 + i;
             if (p >= ((f + cnt[b]) & ~(L - 1))) continue;   // line still incomplete: stays
             const u64 o = slot(b, p);
-            if (o != ~0ull) out[o] = tail[q];
+            if ((ABL & 4) == 0 && o != ~0ull) out[o] = tail[q];
         }
         __syncthreads();
 #pragma unroll

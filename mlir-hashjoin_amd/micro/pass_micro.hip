@@ -61,14 +61,22 @@ int main() {
         ms /= 5;
         printf("%-40s %7.3f ms  %7.1f GB/s (32 B/row)\n", name, ms, 32.0 * n / ms / 1e6);
     };
-    for (int fb : {9, 8}) {
+    for (int fb : {9}) {
         a.fbits = fb;
         a.shift = 64 - fb;
-        for (int pbl : {9, 8}) {
+        for (int pbl : {9}) {
             a.out_pbl = pbl;
             char nm[64];
             snprintf(nm, sizeof nm, "F%d PB%d k_pass", 1 << fb, 1 << pbl);
             run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow>), dim3(grid), dim3(kPassThreads), 0, 0, a); });
+#define P(ABL, TXT)                                                                                       \
+    snprintf(nm, sizeof nm, "F%d PB%d %s", 1 << fb, 1 << pbl, TXT);                                       \
+    run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a); })
+            P(1, "no bucket atomic");
+            P(2, "synthetic rows");
+            P(4, "no row stores");
+            P(6, "synthetic rows, no stores");
+#undef P
         }
     }
     return 0;
