@@ -212,6 +212,7 @@ struct PassArgs {
     int out_pbl;
     int shift;                   // bin = (hash >> shift) & (F - 1)
     int fbits;
+    u64 *prof = nullptr;         // diagnostics (ABL & 8): per workgroup, cycles per phase
 };
 
 struct PassTile {
@@ -281,7 +282,8 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, u
 // open bucket is ever written partly (at close).
 // ABL (diagnostics only, micro/pass_micro.hip; the product uses 0): 1 fresh
 // buckets from a fixed per-tile range instead of the global atomic, 2
-// synthetic rows instead of loads, 4 no row stores (rows and tails).
+// synthetic rows instead of loads, 4 no row stores (rows and tails), 8 time
+// the phases (s_memtime after each barrier, summed into a.prof).
 template <bool WIDE, int FORM, int ABL = 0>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
@@ -374,7 +376,16 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         tl = pass_tile<FORM>(a, t0);
         load_tile(tl, row, br);
     }
+    u64 ph[6] = {0, 0, 0, 0, 0, 0}, tp = 0;
+    auto mark = [&](int k) {
+        if constexpr ((ABL & 8) != 0) {
+            const u64 now = __builtin_amdgcn_s_memtime();
+            if (k >= 0) ph[k] += now - tp;
+            tp = now;
+        }
+    };
     for (unsigned t = t0; t < t1; ++t) {
+        mark(-1);
         if (tl.seg != seg_cur) {   // uniform: every thread sees the same tile
             __syncthreads();
             close_all();
@@ -388,6 +399,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             br[i] = (b << 16) | atomicAdd(&cnt[b], 1u);
         }
         __syncthreads();
+        mark(0);
         if (threadIdx.x < 64) {
             // wave 0: exclusive scans of the bin counts (-> start) and of the
             // fresh buckets each bin needs (-> nbase, relative); ONE global
@@ -431,6 +443,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             }
         }
         __syncthreads();
+        mark(1);
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
             if (br[i] == 0xFFFFFFFFu) continue;
@@ -440,6 +453,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             sb[pos] = (unsigned short)b;
         }
         __syncthreads();
+        mark(2);
         // the next tile's loads are in flight during this tile's stores
         const int seg = tl.seg;
         if (t + 1 < t1) {
@@ -476,6 +490,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             if ((ABL & 4) == 0 && o != ~0ull) out[o] = tail[q];
         }
         __syncthreads();
+        mark(3);
 #pragma unroll
         for (int i = 0; i < IT; ++i)
             if (tpos[i] != 0xFFFFFFFFu) tail[tpos[i]] = stage[(unsigned)i * kPassThreads + threadIdx.x];
@@ -506,8 +521,13 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             }
         }
         __syncthreads();
+        mark(4);
     }
     close_all();
+    if constexpr ((ABL & 8) != 0) {
+        if (threadIdx.x == 0 && a.prof)
+            for (int k = 0; k < 6; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
+    }
 }
 
 // Bucket list by partition: count buckets per partition, exclusive scan

@@ -7,6 +7,7 @@
 #include "../csrc/hj_radix.hip"
 
 #include <cstdio>
+#include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace hj;
@@ -77,6 +78,29 @@ int main() {
             P(4, "no row stores");
             P(6, "synthetic rows, no stores");
 #undef P
+            // phase times (cycles of s_memtime, summed over a workgroup's tiles, mean over workgroups)
+            u64 *prof;
+            CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
+            CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
+            a.prof = prof;
+            CK(hipMemset(nb, 0, 4));
+            hipLaunchKernelGGL((k_pass<true, kPackedRow, 8>), dim3(grid), dim3(kPassThreads), 0, 0, a);
+            CK(hipDeviceSynchronize());
+            std::vector<u64> h(grid * 8);
+            CK(hipMemcpy(h.data(), prof, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
+            const char *names[6] = {"load wait + hash + LDS count", "scan + bucket atomic", "LDS scatter",
+                                    "next loads issued + stores + tails", "new tails + bookkeeping", "-"};
+            double tot = 0;
+            double m[6];
+            for (int k = 0; k < 5; ++k) {
+                double acc = 0;
+                for (unsigned g = 0; g < grid; ++g) acc += (double)h[g * 8 + k];
+                m[k] = acc / grid;
+                tot += m[k];
+            }
+            for (int k = 0; k < 5; ++k) printf("  phase %-38s %10.0f cycles  %5.1f %%\n", names[k], m[k], 100.0 * m[k] / tot);
+            a.prof = nullptr;
+            CK(hipFree(prof));
         }
     }
     return 0;
