@@ -293,7 +293,8 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ T stage[kTile];
     __shared__ T tail[kMaxFan * (L - 1)];   // bin b: rows of positions [fill & ~(L-1), fill)
     __shared__ unsigned short sb[kTile];
-    __shared__ unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan], nbase[kMaxFan];
+    __shared__ __attribute__((aligned(16))) unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan],
+        nbase[kMaxFan];
     __shared__ unsigned s_nb;   // first fresh bucket of the current tile
     const unsigned F = 1u << a.fbits;
     const unsigned PB = 1u << a.out_pbl;
@@ -406,14 +407,21 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             // atomic reserves the tile's buckets (a counter hit once per bin
             // allocation serialised ~1M atomics per 2^28-row pass)
             const int lane = threadIdx.x;
+            // (8 bins per lane moved as two 16-B LDS accesses per array:
+            // wave 0 alone is on the critical path here)
             unsigned c[8], k[8], s = 0, sk = 0;
+            {
+                const uint4 c0 = ((const uint4 *)cnt)[lane * 2], c1 = ((const uint4 *)cnt)[lane * 2 + 1];
+                const uint4 f0 = ((const uint4 *)fill)[lane * 2], f1 = ((const uint4 *)fill)[lane * 2 + 1];
+                const unsigned cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+                const unsigned fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const unsigned b = lane * 8 + j;
-                c[j] = b < F ? cnt[b] : 0u;
-                k[j] = c[j] ? (fill[b] + c[j] - 1) >> a.out_pbl : 0u;
-                s += c[j];
-                sk += k[j];
+                for (int j = 0; j < 8; ++j) {
+                    c[j] = lane * 8 + j < F ? cv[j] : 0u;
+                    k[j] = c[j] ? (fv[j] + c[j] - 1) >> a.out_pbl : 0u;
+                    s += c[j];
+                    sk += k[j];
+                }
             }
             unsigned x = s, xk = sk;
 #pragma unroll
@@ -425,15 +433,19 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 }
             }
             unsigned run = x - s, runk = xk - sk;
+            unsigned sv[8], nv[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const unsigned b = lane * 8 + j;
-                if (b < F) {
-                    start[b] = run;
-                    nbase[b] = runk;
-                }
+                sv[j] = run;
+                nv[j] = runk;
                 run += c[j];
                 runk += k[j];
+            }
+            if (lane * 8 < F) {   // (entries of bins >= F are written but never read)
+                ((uint4 *)start)[lane * 2] = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+                ((uint4 *)start)[lane * 2 + 1] = make_uint4(sv[4], sv[5], sv[6], sv[7]);
+                ((uint4 *)nbase)[lane * 2] = make_uint4(nv[0], nv[1], nv[2], nv[3]);
+                ((uint4 *)nbase)[lane * 2 + 1] = make_uint4(nv[4], nv[5], nv[6], nv[7]);
             }
             if (lane == 63) {
                 unsigned nb = (ABL & 1) ? (unsigned)(((u64)tl.lo / kTile * 24u) % (a.max_buckets - 1024u))

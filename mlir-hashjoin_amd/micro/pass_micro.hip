@@ -8,6 +8,9 @@
 
 #include <cstdio>
 #include <vector>
+#ifndef PHASE_ABL
+#define PHASE_ABL 8
+#endif
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 using namespace hj;
@@ -84,7 +87,7 @@ int main() {
             CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
             a.prof = prof;
             CK(hipMemset(nb, 0, 4));
-            hipLaunchKernelGGL((k_pass<true, kPackedRow, 8>), dim3(grid), dim3(kPassThreads), 0, 0, a);
+            hipLaunchKernelGGL((k_pass<true, kPackedRow, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a);
             CK(hipDeviceSynchronize());
             std::vector<u64> h(grid * 8);
             CK(hipMemcpy(h.data(), prof, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
