@@ -401,6 +401,13 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(0);
+        // the next tile's loads are in flight from here on (through the
+        // scan, the LDS scatter and this tile's stores)
+        const int seg = tl.seg;
+        T nrow[IT];
+        unsigned nbr[IT];
+        const PassTile ntl = t + 1 < t1 ? pass_tile<FORM>(a, t + 1) : tl;
+        if (t + 1 < t1) load_tile(ntl, nrow, nbr);
         if (threadIdx.x < 64) {
             // wave 0: exclusive scans of the bin counts (-> start) and of the
             // fresh buckets each bin needs (-> nbase, relative); ONE global
@@ -466,12 +473,6 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(2);
-        // the next tile's loads are in flight during this tile's stores
-        const int seg = tl.seg;
-        if (t + 1 < t1) {
-            tl = pass_tile<FORM>(a, t + 1);
-            load_tile(tl, row, br);
-        }
         // Bin b's rows now span positions [fill, fill + cnt) of its bucket
         // run; lines end below E = (fill + cnt) & ~(L - 1).  Rows below E
         // are stored (the tail's first), the rest become the new tail.
@@ -534,6 +535,12 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(4);
+        tl = ntl;
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            row[i] = nrow[i];
+            br[i] = nbr[i];
+        }
     }
     close_all();
     if constexpr ((ABL & 8) != 0) {
