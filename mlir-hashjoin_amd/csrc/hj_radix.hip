@@ -53,6 +53,10 @@ constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
 constexpr int kPassPbl = 9;        // 512-row buckets for intermediate passes
 constexpr int kFinalPbl = 8;       // 256-row buckets for the join's input (less slack)
+#ifndef HJ_POOL_BUCKETS
+#define HJ_POOL_BUCKETS 64
+#endif
+constexpr unsigned kPoolBuckets = HJ_POOL_BUCKETS;   // bucket ids a pass workgroup reserves per global atomic
 
 __device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
 
@@ -295,7 +299,10 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ unsigned short sb[kTile];
     __shared__ __attribute__((aligned(16))) unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan],
         nbase[kMaxFan];
-    __shared__ unsigned s_nb;   // first fresh bucket of the current tile
+    // the tile's fresh buckets: s_nrem from s_nb (the pool's rest), then
+    // from s_nb2 (a refill); kNoBucket when the set is exhausted
+    __shared__ unsigned s_nb, s_nrem, s_nb2;
+    __shared__ unsigned s_hole[2];
     const unsigned F = 1u << a.fbits;
     const unsigned PB = 1u << a.out_pbl;
     const unsigned T_ = pass_tiles<FORM>(a);
@@ -307,11 +314,19 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         cur[b] = kNoBucket;
         fill[b] = PB;   // no open bucket (and no tail: PB is a whole number of lines)
     }
+    // the tile's x-th fresh bucket
+    auto fresh = [&](unsigned x) -> unsigned {
+        return x < s_nrem ? s_nb + x : (s_nb2 == kNoBucket ? kNoBucket : s_nb2 + (x - s_nrem));
+    };
+    // fresh buckets are taken from a per-workgroup pool of kPoolBuckets ids
+    // (wave 0, lane 63): one returning global atomic per refill instead of
+    // one per tile, which stalled the workgroup at every tile's scan
+    unsigned pool_lo = 0u, pool_hi = 0u;
     // row slot of position p (>= the line start of fill[b]) of bin b's run
     // in the current tile: the open bucket, then the tile's fresh buckets
     auto slot = [&](unsigned b, unsigned p) -> u64 {
         const unsigned k = p >> a.out_pbl;
-        const unsigned bk = k == 0 ? cur[b] : (s_nb == kNoBucket ? kNoBucket : s_nb + nbase[b] + k - 1);
+        const unsigned bk = k == 0 ? cur[b] : fresh(nbase[b] + k - 1);
         return bk < a.max_buckets ? ((u64)bk << a.out_pbl) + (p & (PB - 1)) : ~0ull;
     };
     int seg_cur = -1;
@@ -455,10 +470,27 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 ((uint4 *)nbase)[lane * 2 + 1] = make_uint4(nv[4], nv[5], nv[6], nv[7]);
             }
             if (lane == 63) {
-                unsigned nb = (ABL & 1) ? (unsigned)(((u64)tl.lo / kTile * 24u) % (a.max_buckets - 1024u))
-                                        : (xk ? atomicAdd(a.nb, xk) : 0u);
-                if ((u64)nb + xk > a.max_buckets) nb = kNoBucket;   // cannot happen within radix_need
-                s_nb = nb;
+                const unsigned rem = pool_hi - pool_lo;
+                s_nb = pool_lo;
+                s_nrem = xk < rem ? xk : rem;
+                s_nb2 = kNoBucket;
+                if (xk <= rem) {
+                    pool_lo += xk;
+                } else {
+                    // refill: the tile takes the pool's rest, then the start
+                    // of a new reservation (a set out of buckets cannot
+                    // happen within radix_need; such rows are dropped)
+                    const unsigned need = xk - rem, take = need > kPoolBuckets ? need : kPoolBuckets;
+                    const unsigned nb = (ABL & 1) ? (unsigned)(((u64)tl.lo / kTile * 24u) % (a.max_buckets - 1024u))
+                                                  : atomicAdd(a.nb, take);
+                    if ((u64)nb + take <= a.max_buckets) {
+                        s_nb2 = nb;
+                        pool_lo = nb + need;
+                        pool_hi = nb + take;
+                    } else {
+                        pool_lo = pool_hi = 0u;
+                    }
+                }
             }
         }
         __syncthreads();
@@ -517,17 +549,14 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 // the replaced open bucket is full (all its lines stored);
                 // record the fresh ones
                 if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
-                if (s_nb != kNoBucket) {
-                    const unsigned nb = s_nb + nbase[b];
-                    const unsigned pid = ((unsigned)seg << a.fbits) | b;
-                    for (unsigned i = 0; i < k; ++i) {
-                        a.bbin[nb + i] = pid;
-                        if (i + 1 < k) a.bfill[nb + i] = PB;
-                    }
-                    cur[b] = nb + k - 1;
-                } else {
-                    cur[b] = kNoBucket;
+                const unsigned pid = ((unsigned)seg << a.fbits) | b;
+                for (unsigned i = 0; i < k; ++i) {
+                    const unsigned bk = fresh(nbase[b] + i);
+                    if (bk == kNoBucket) continue;
+                    a.bbin[bk] = pid;
+                    if (i + 1 < k) a.bfill[bk] = PB;
                 }
+                cur[b] = fresh(nbase[b] + k - 1);
                 fill[b] = f + c - (k << a.out_pbl);
             } else {
                 fill[b] = f + c;
@@ -543,6 +572,12 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
     }
     close_all();
+    if (threadIdx.x == 63) {
+        s_hole[0] = pool_lo;
+        s_hole[1] = pool_hi;
+    }
+    __syncthreads();
+    for (unsigned i = s_hole[0] + threadIdx.x; i < s_hole[1]; i += kPassThreads) a.bbin[i] = kNoBucket;
     if constexpr ((ABL & 8) != 0) {
         if (threadIdx.x == 0 && a.prof)
             for (int k = 0; k < 6; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
@@ -570,9 +605,10 @@ __global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const uns
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
-        if (j < n) {
-            if (lds) atomicAdd(&c[bbin[j]], 1u);
-            else atomicAdd(&pcnt[bbin[j]], 1ull);
+        const unsigned b = j < n ? bbin[j] : kNoBucket;
+        if (b < (unsigned)P) {   // holes (unused pool ids) are kNoBucket
+            if (lds) atomicAdd(&c[b], 1u);
+            else atomicAdd(&pcnt[b], 1ull);
         }
     }
     if (!lds) return;
@@ -592,7 +628,8 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
 #pragma unroll
         for (int i = 0; i < kListPer; ++i) {
             const u64 j = base + (u64)i * 1024 + threadIdx.x;
-            if (j < n) blist[atomicAdd(&pcur[bbin[j]], 1ull)] = (j << 32) | bfill[j];
+            const unsigned b = j < n ? bbin[j] : kNoBucket;
+            if (b < (unsigned)P) blist[atomicAdd(&pcur[b], 1ull)] = (j << 32) | bfill[j];
         }
         return;
     }
@@ -603,6 +640,7 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         bn[i] = j < n ? bbin[j] : kNoBucket;
+        if (bn[i] >= (unsigned)P) bn[i] = kNoBucket;
         if (bn[i] != kNoBucket) rk[i] = atomicAdd(&c[bn[i]], 1u);
     }
     __syncthreads();
@@ -1100,7 +1138,8 @@ RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
         const u64 F = 1ull << pl.bits[i];
         // every bucket holds >= 1 row, so never more than `rows` buckets
         const u64 open = ((u64)pass_grid(rows) + nseg + 1) * F;
-        const u64 b = (rows >> pl.pbl[i]) + (open < rows ? open : rows) + 1;
+        const u64 holes = (u64)pass_grid(rows) * kPoolBuckets;   // each workgroup's unused pool rest
+        const u64 b = (rows >> pl.pbl[i]) + (open < rows ? open : rows) + holes + 1;
         if (to_final == final_set) {
             if (b > need.buckets) need.buckets = b;
             if ((b << pl.pbl[i]) > need.rows) need.rows = b << pl.pbl[i];
