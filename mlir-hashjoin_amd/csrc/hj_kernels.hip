@@ -281,16 +281,17 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
         for (int i = 0; i < kProbeItems; ++i) {
             RP[i] = 0;
             if (!V[i]) continue;
+            // duplicate-free table: the chain ends at the match or at EMPTY
+            // (a two-exit loop with nothing else in it)
             slot_t sv = S[i];
             unsigned long long hh = H[i];
-            while (!LY::empty(sv)) {
-                if (LY::key(sv) == K[i]) {
-                    found |= 1u << i;
-                    RP[i] = LY::pay(sv);
-                    break;
-                }
+            while (!LY::empty(sv) && LY::key(sv) != K[i]) {
                 hh = (hh + 1) & t.mask;
                 sv = sl[hh];
+            }
+            if (!LY::empty(sv)) {
+                found |= 1u << i;
+                RP[i] = LY::pay(sv);
             }
         }
         if constexpr (!WRITE) {
