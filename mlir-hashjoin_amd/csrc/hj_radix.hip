@@ -871,20 +871,38 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                     // duplicate-free build: a row's chain ends at its match
                     // or at EMPTY -- a two-exit loop with nothing else in it
                     // (the general loop below costs ~3x per step)
+                    // Row slots walk in pairs: one loop advances both chains,
+                    // two LDS reads in flight per step, and the wave waits
+                    // for the longest chain of each pair instead of each slot
+                    auto open = [&](u64 e, u64 key) { return e != kEmpty && (WIDE ? e : (e >> 32)) != key; };
 #pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if (!pa[i]) continue;
-                        const u64 key = R::key(sv_[i]);
-                        unsigned h = hp[i];
-                        u64 e = e0[i];
-                        while (e != kEmpty && (WIDE ? e : (e >> 32)) != key) {
+                    for (int i = 0; i < SI; i += 2) {
+                        const int j = i + 1 < SI ? i + 1 : i;
+                        const u64 ka = R::key(sv_[i]), kb = R::key(sv_[j]);
+                        unsigned ha = hp[i], hb = hp[j];
+                        u64 ea = e0[i], eb = e0[j];
+                        bool la = pa[i] && open(ea, ka);
+                        bool lb = j != i && pa[j] && open(eb, kb);
+                        while (la || lb) {
                             if constexpr ((ABL & 16) != 0) break;
-                            h = (h + 1) & kMask;
-                            e = tkey[h];
+                            if (la) {
+                                ha = (ha + 1) & kMask;
+                                ea = tkey[ha];
+                            }
+                            if (lb) {
+                                hb = (hb + 1) & kMask;
+                                eb = tkey[hb];
+                            }
+                            la = la && open(ea, ka);
+                            lb = lb && open(eb, kb);
                         }
-                        if (e != kEmpty && (WIDE ? e : (e >> 32)) == key) {
+                        if (pa[i] && ea != kEmpty && (WIDE ? ea : (ea >> 32)) == ka) {
                             ++cnt;
-                            m[i] = h;
+                            m[i] = ha;
+                        }
+                        if (j != i && pa[j] && eb != kEmpty && (WIDE ? eb : (eb >> 32)) == kb) {
+                            ++cnt;
+                            m[j] = hb;
                         }
                     }
                 } else {
