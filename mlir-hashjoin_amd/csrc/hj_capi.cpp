@@ -87,9 +87,10 @@ struct Buf {
 
 // Device buffers of one radix bucket set (hj::BucketSet).
 struct SetBufs {
-    Buf rows, bbin, bfill, blist, pstart;
+    Buf rows, bbin, bfill, blist, pstart, runs, rstart;
     unsigned max_buckets = 0;
     unsigned long long max_rows = 0;
+    unsigned long long max_runs = 0;
 };
 
 }  // namespace
@@ -113,7 +114,7 @@ struct hj_ctx {
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
-    Buf nb, pcur, tile_start, tile_owner, work_start, work_desc, scan_sums;
+    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, work_start, work_desc, scan_sums;
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
@@ -206,12 +207,16 @@ int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
     HJ_TRY(ensure_buf(sb.bfill, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.blist, (size_t)need.buckets * 8));
     HJ_TRY(ensure_buf(sb.pstart, (P + 1) * 8));
+    HJ_TRY(ensure_buf(sb.rstart, (P + 1) * 8));
     // capacity actually held (buffers may be larger than this need)
     size_t cap = sb.bbin.bytes / 4;
     if (sb.bfill.bytes / 4 < cap) cap = sb.bfill.bytes / 4;
     if (sb.blist.bytes / 8 < cap) cap = sb.blist.bytes / 8;
     sb.max_buckets = (unsigned)(cap < 0xFFFFFFF0ull ? cap : 0xFFFFFFF0ull);
     sb.max_rows = sb.rows.bytes / esz;
+    // a bucket of f rows lists ceil(f / 64) runs: <= rows / 64 + buckets
+    HJ_TRY(ensure_buf(sb.runs, (size_t)((sb.max_rows >> hj::kRunLog) + sb.max_buckets) * 8));
+    sb.max_runs = sb.runs.bytes / 8;
     return HJ_OK;
 }
 
@@ -222,8 +227,11 @@ hj::BucketSet bucket_set(SetBufs &sb) {
     b.bfill = (unsigned *)sb.bfill.p;
     b.blist = (unsigned long long *)sb.blist.p;
     b.pstart = (unsigned long long *)sb.pstart.p;
+    b.runs = (unsigned long long *)sb.runs.p;
+    b.rstart = (unsigned long long *)sb.rstart.p;
     b.max_buckets = sb.max_buckets;
     b.max_rows = sb.max_rows;
+    b.max_runs = sb.max_runs;
     return b;
 }
 
@@ -235,10 +243,12 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     if (pl.passes > 1) HJ_TRY(ensure_set(c->tset, hj::radix_need(n, pl, false), esz, P));
     HJ_TRY(ensure_buf(c->nb, 16));
     HJ_TRY(ensure_buf(c->pcur, (P + 1) * 8));
+    HJ_TRY(ensure_buf(c->rcur, (P + 1) * 8));
     HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
     HJ_TRY(ensure_buf(c->tile_owner, (size_t)hj::radix_tiles(n, (int)P) * 4));
+    HJ_TRY(ensure_buf(c->tdesc, (size_t)hj::radix_tiles(n, (int)P) * 16));
     // work map: P + 1 chunk starts, then the item -> partition owner list
-    const size_t items = (size_t)hj::radix_join_items(pl, fin.max_buckets);
+    const size_t items = (size_t)hj::radix_join_items(pl, fin.max_runs);
     HJ_TRY(ensure_buf(c->work_start, (P + 1 + items) * 4));
     HJ_TRY(ensure_buf(c->work_desc, items * hj::radix_item_desc_bytes()));
     HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
@@ -250,8 +260,10 @@ hj::RadixWork radix_work(hj_ctx *c) {
     w.tmp = bucket_set(c->tset);
     w.nb = (unsigned *)c->nb.p;
     w.pcur = (unsigned long long *)c->pcur.p;
+    w.rcur = (unsigned long long *)c->rcur.p;
     w.tile_start = (unsigned *)c->tile_start.p;
     w.tile_owner = (unsigned *)c->tile_owner.p;
+    w.tdesc = c->tdesc.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
     return w;
 }
@@ -351,7 +363,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
-        HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_buckets,
+        HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
                               (unsigned long long *)d_count, c->meta + 1, count_only, st));
         trace("probe: joined", st, cap);
@@ -793,8 +805,8 @@ void hj_ctx_destroy(hj_ctx *c) {
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
-        for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->tile_start, &c->tile_owner, &c->work_start, &c->work_desc, &c->scan_sums,
+        for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart, &sb->runs, &sb->rstart}) free_buf(*b);
+    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->work_start, &c->work_desc, &c->scan_sums,
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums})
         free_buf(*b);
     if (c->ev_ready)

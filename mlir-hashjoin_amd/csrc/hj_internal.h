@@ -93,22 +93,32 @@ struct RadixPlan {
 // One pass's output: packed rows in buckets of 2^pbl rows; bucket j holds
 // bfill[j] rows of partition bbin[j].  After the pass, blist lists the
 // buckets grouped by partition as (j << 32 | bfill[j]): partition p owns
-// blist[pstart[p] .. pstart[p+1]).
+// blist[pstart[p] .. pstart[p+1]).  The same rows are also listed as RUNS
+// of <= 64 consecutive rows of one bucket (row << 7 | count; a bucket of f
+// rows gives ceil(f / 64) runs), grouped by partition: p owns
+// runs[rstart[p] .. rstart[p+1]).  Consumers that map one wave to 64 rows
+// read runs, so a partly filled bucket idles at most one wave's tail.
+constexpr int kRunLog = 6;
 struct BucketSet {
     void *rows;                    // >= max_buckets << pbl rows
     unsigned *bbin, *bfill;        // >= max_buckets
     unsigned long long *blist;     // >= max_buckets
     unsigned long long *pstart;    // >= P + 1 (P of the pass writing the set)
+    unsigned long long *runs;      // >= max_runs
+    unsigned long long *rstart;    // >= P + 1
     unsigned max_buckets;          // bbin / bfill / blist entries
     unsigned long long max_rows;   // rows entries
+    unsigned long long max_runs;   // runs entries (max_rows / 64 + max_buckets covers any fill)
 };
 
 struct RadixWork {                 // scratch shared by the partition passes
     BucketSet tmp;                 // ping set of multi-pass plans
     unsigned *nb;                  // device bucket counter
     unsigned long long *pcur;      // >= P + 1: list placement cursors / chunk-map scratch
+    unsigned long long *rcur;      // >= P + 1: run placement cursors
     unsigned *tile_start;          // >= P + 1
     unsigned *tile_owner;          // >= radix_tiles(n, P)
+    void *tdesc;                   // >= radix_tiles(n, P) * 16 B: bucketed-pass tile descriptors
     unsigned long long *scan_sums; // >= P / 8192 + 2
 };
 
@@ -120,14 +130,14 @@ RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0
 // Bucket capacity of the final set (`final_set`) or the ping set of plan pl for n rows.
 RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set);
 unsigned long long radix_tiles(long long n, int max_nseg);
-unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets);
+unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs);
 // Partitioned rows are packed: 16 B {key, pay} (wide) or 8 B key << 32 | row id (narrow).
 hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
                            const BucketSet &out, hipStream_t st);
 size_t radix_item_desc_bytes();
 // work_start: >= P + 1 + radix_join_items words; desc: >= radix_join_items * radix_item_desc_bytes()
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
-                      unsigned s_buckets, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
+                      unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st);
 
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,

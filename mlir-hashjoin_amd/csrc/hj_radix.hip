@@ -202,12 +202,13 @@ struct PassArgs {
     u64 n;                       // pass-1 source rows
     bool cols_aligned;           // kCols64: both columns 16-B aligned
     // FORM == kBucketed: the previous pass's set, tiles of up to kTile rows
-    // (kTile >> kPassPbl buckets) that never straddle two segments
+    // (kTile >> kRunLog runs) that never straddle two segments
     const void *in_rows;
-    const u64 *in_list;          // bucket << 32 | fill
-    const u64 *in_pstart;
+    const u64 *in_runs;          // row << 7 | count
+    const u64 *in_rstart;
+    u64 in_max_rows, in_max_runs;   // capacities of the input set (loads are clamped to them)
     const unsigned *tile_start;  // nseg + 1
-    const unsigned *tile_owner;  // tile -> segment
+    const struct TileDesc *tdesc;   // per tile (k_tile_desc)
     int nseg;
     // output set
     void *out_rows;
@@ -219,10 +220,25 @@ struct PassArgs {
     u64 *prof = nullptr;         // diagnostics (ABL & 8): per workgroup, cycles per phase
 };
 
-struct PassTile {
-    int seg;
-    u64 lo, hi;                  // source rows, or bucket-list positions (kBucketed)
+// A bucketed pass's tile: runs [lo, lo + cnt) (cnt <= kTile / 64) of segment seg.
+struct TileDesc {
+    u64 lo;
+    unsigned cnt, seg;
 };
+
+__global__ __launch_bounds__(256) void k_tile_desc(const unsigned *tile_start, const unsigned *tile_owner,
+                                                   const u64 *rstart, int nseg, unsigned bound, TileDesc *desc) {
+    const unsigned t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= tile_start[nseg] || t >= bound) return;
+    const unsigned seg = tile_owner[t];
+    const u64 lo = rstart[seg] + (u64)(t - tile_start[seg]) * (unsigned)(kTile >> kRunLog);
+    const u64 e = rstart[seg + 1];
+    TileDesc d;
+    d.lo = lo;
+    d.cnt = (unsigned)(e - lo < (u64)(kTile >> kRunLog) ? e - lo : (u64)(kTile >> kRunLog));
+    d.seg = seg;
+    desc[t] = d;
+}
 
 template <int FORM>
 __device__ __forceinline__ unsigned pass_tiles(const PassArgs &a) {
@@ -230,44 +246,14 @@ __device__ __forceinline__ unsigned pass_tiles(const PassArgs &a) {
     else return (unsigned)((a.n + kTile - 1) / kTile);
 }
 
-template <int FORM>
-__device__ __forceinline__ PassTile pass_tile(const PassArgs &a, unsigned t) {
-    PassTile r;
-    if constexpr (FORM == kBucketed) {
-        r.seg = a.nseg == 1 ? 0 : (int)a.tile_owner[t];
-        const unsigned bpt = (unsigned)kTile >> kPassPbl;
-        r.lo = a.in_pstart[r.seg] + (u64)(t - a.tile_start[r.seg]) * bpt;
-        const u64 e = a.in_pstart[r.seg + 1];
-        r.hi = r.lo + bpt < e ? r.lo + bpt : e;
-    } else {
-        r.seg = 0;
-        r.lo = (u64)t * kTile;
-        r.hi = r.lo + kTile < a.n ? r.lo + kTile : a.n;
-    }
-    return r;
-}
-
-// Row v (0 <= v < kTile) of a tile; false if the tile has no such row.
+// Row v (0 <= v < kTile) of the row-source tile starting at row lo; false
+// if the source has no such row.
 template <bool WIDE, int FORM>
-__device__ __forceinline__ bool tile_row(const PassArgs &a, const PassTile &t, unsigned v, typename Row<WIDE>::T &out) {
-    typedef Row<WIDE> R;
-    if constexpr (FORM == kBucketed) {
-        // input buckets are kPassPbl rows and a wave's 64 lanes share one:
-        // the list entry is wave-uniform (scalar load, SGPRs)
-        static_assert((kPassThreads >> kPassPbl) >= 1, "a wave must stay inside one bucket");
-        const u64 li = t.lo + __builtin_amdgcn_readfirstlane(v >> kPassPbl);
-        if (li >= t.hi) return false;
-        const u64 e = a.in_list[li];
-        const unsigned off = v & ((1u << kPassPbl) - 1u);
-        if (off >= (unsigned)e) return false;
-        out = ((const typename R::T *)a.in_rows)[((e >> 32) << kPassPbl) + off];
-        return true;
-    } else {
-        const u64 row = t.lo + v;
-        if (row >= t.hi) return false;
-        out = load_row<WIDE, FORM>(a.in, (long long)row);
-        return true;
-    }
+__device__ __forceinline__ bool tile_row(const PassArgs &a, u64 lo, unsigned v, typename Row<WIDE>::T &out) {
+    const u64 row = lo + v;
+    if (row >= a.n) return false;
+    out = load_row<WIDE, FORM>(a.in, (long long)row);
+    return true;
 }
 
 // One partition pass (see the file header).  Workgroup w owns tiles
@@ -344,11 +330,11 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
     };
     // rows of tile tl into registers (br = 0 valid, ~0 none)
-    auto load_tile = [&](const PassTile &tl, T (&row)[IT], unsigned (&br)[IT]) {
+    auto load_tile = [&](u64 tlo, T (&row)[IT], unsigned (&br)[IT]) {
         if constexpr ((ABL & 2) != 0) {
 #pragma unroll
             for (int i = 0; i < IT; ++i) {
-                const u64 v = tl.lo * 7 + (u64)i * kPassThreads + threadIdx.x;
+                const u64 v = tlo * 7 + (u64)i * kPassThreads + threadIdx.x;
                 row[i] = R::make(fmix64(v), v);
                 br[i] = 0u;
             }
@@ -358,25 +344,26 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const u64 *kc = (const u64 *)a.in.key, *pc = (const u64 *)a.in.pay;
 #pragma unroll
             for (int i = 0; i < IT / 2; ++i) {
-                const u64 r = tl.lo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
-                if (a.cols_aligned && r + 1 < tl.hi) {
+                const u64 r = tlo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
+                const bool v0 = r < a.n, v1 = r + 1 < a.n;
+                if (a.cols_aligned && v1) {
                     const ulonglong2 k2 = *(const ulonglong2 *)(kc + r);
                     const ulonglong2 p2 = *(const ulonglong2 *)(pc + r);
                     row[2 * i] = R::make(k2.x, p2.x);
                     row[2 * i + 1] = R::make(k2.y, p2.y);
-                    br[2 * i] = br[2 * i + 1] = 0u;
                 } else {
-                    const bool v0 = r < tl.hi, v1 = r + 1 < tl.hi;
                     row[2 * i] = v0 ? R::make(kc[r], pc[r]) : R::zero();
                     row[2 * i + 1] = v1 ? R::make(kc[r + 1], pc[r + 1]) : R::zero();
-                    br[2 * i] = v0 ? 0u : 0xFFFFFFFFu;
-                    br[2 * i + 1] = v1 ? 0u : 0xFFFFFFFFu;
                 }
+                // (one assignment per element: stores in both branches made
+                // the compiler keep br in scratch memory)
+                br[2 * i] = v0 ? 0u : 0xFFFFFFFFu;
+                br[2 * i + 1] = v1 ? 0u : 0xFFFFFFFFu;
             }
-        } else {
+        } else if constexpr (FORM != kBucketed) {
 #pragma unroll
             for (int i = 0; i < IT; ++i) {
-                if (!tile_row<WIDE, FORM>(a, tl, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
+                if (!tile_row<WIDE, FORM>(a, tlo, (unsigned)i * kPassThreads + threadIdx.x, row[i])) {
                     row[i] = R::zero();
                     br[i] = 0xFFFFFFFFu;
                 } else {
@@ -385,12 +372,59 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             }
         }
     };
+    // FORM == kBucketed: row v of a tile is row v % 64 of the tile's run
+    // v / 64 (a wave's 64 lanes read one run, <= 64 rows of one bucket, so a
+    // partly filled bucket idles at most its last run's tail).  Tile t's rows
+    // are loaded in iteration t - 1 from its run entries (lane j holds entry
+    // j), loaded in iteration t - 2 from its descriptor, loaded in iteration
+    // t - 3: each load waits only on data that was in flight for a whole
+    // tile.  (Issued back to back, the chain descriptor -> entry -> row cost
+    // several memory latencies per tile: 2.23 ms for pass 2 vs 1.89 ms for
+    // pass 1, profiles/r01_micro_pass2.txt.)
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    auto get_desc = [&](unsigned t) -> ulonglong2 {
+        return t < t1 ? *(const ulonglong2 *)&a.tdesc[t] : make_ulonglong2(0ull, 0ull);
+    };
+    auto get_ents = [&](const ulonglong2 &d) -> u64 {
+        return lane < (unsigned)d.y && d.x + lane < a.in_max_runs ? a.in_runs[d.x + lane] : 0ull;
+    };
+    auto rows_from = [&](u64 ent, T (&row)[IT], unsigned (&br)[IT]) {
+        const unsigned elo = (unsigned)ent, ehi = (unsigned)(ent >> 32);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const unsigned src = (unsigned)i * (kPassThreads >> kRunLog) + wave;   // run of this row slot
+            // (readlane returns int: widen through unsigned, not sign-extended)
+            const u64 e = ((u64)(unsigned)__builtin_amdgcn_readlane(ehi, src) << 32) |
+                          (u64)(unsigned)__builtin_amdgcn_readlane(elo, src);
+            if (lane < (unsigned)(e & 127u) && (e >> 7) + lane < a.in_max_rows) {
+                row[i] = ((const T *)a.in_rows)[(e >> 7) + lane];
+                br[i] = 0u;
+            } else {
+                row[i] = R::zero();
+                br[i] = 0xFFFFFFFFu;
+            }
+        }
+    };
+    auto seg_of = [&](const ulonglong2 &d) -> int { return (int)__builtin_amdgcn_readfirstlane((unsigned)(d.y >> 32)); };
     T row[IT];
     unsigned br[IT];   // bin << 16 | rank within the tile's bin
-    PassTile tl{};
+    u64 tlo = 0;    // first row of the current tile (row sources)
+    int tseg = 0;   // segment of the current tile (row sources: 0)
+    ulonglong2 dn = make_ulonglong2(0ull, 0ull), dn2 = dn;   // kBucketed: descriptors of tiles t + 1, t + 2
+    u64 en = 0ull;                                            // kBucketed: run entries of tile t + 1
     if (t0 < t1) {
-        tl = pass_tile<FORM>(a, t0);
-        load_tile(tl, row, br);
+        if constexpr (FORM == kBucketed) {
+            const ulonglong2 d0 = get_desc(t0);
+            rows_from(get_ents(d0), row, br);
+            tseg = seg_of(d0);
+            dn = get_desc(t0 + 1);
+            en = get_ents(dn);
+            dn2 = get_desc(t0 + 2);
+        } else {
+            tlo = (u64)t0 * kTile;
+            load_tile(tlo, row, br);
+        }
     }
     u64 ph[6] = {0, 0, 0, 0, 0, 0}, tp = 0;
     auto mark = [&](int k) {
@@ -402,10 +436,10 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     };
     for (unsigned t = t0; t < t1; ++t) {
         mark(-1);
-        if (tl.seg != seg_cur) {   // uniform: every thread sees the same tile
+        if (tseg != seg_cur) {   // uniform: every thread sees the same tile
             __syncthreads();
             close_all();
-            seg_cur = tl.seg;
+            seg_cur = tseg;
             __syncthreads();
         }
 #pragma unroll
@@ -418,11 +452,22 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         mark(0);
         // the next tile's loads are in flight from here on (through the
         // scan, the LDS scatter and this tile's stores)
-        const int seg = tl.seg;
+        const int seg = tseg;
         T nrow[IT];
         unsigned nbr[IT];
-        const PassTile ntl = t + 1 < t1 ? pass_tile<FORM>(a, t + 1) : tl;
-        if (t + 1 < t1) load_tile(ntl, nrow, nbr);
+        int nseg_t = tseg;
+        const u64 ntlo = (u64)(t + 1) * kTile;
+        if constexpr (FORM == kBucketed) {
+            if (t + 1 < t1) {
+                rows_from(en, nrow, nbr);
+                nseg_t = seg_of(dn);
+                dn = dn2;
+                en = get_ents(dn);   // tile t + 2
+                dn2 = get_desc(t + 3);
+            }
+        } else {
+            if (t + 1 < t1) load_tile(ntlo, nrow, nbr);
+        }
         if (threadIdx.x < 64) {
             // wave 0: exclusive scans of the bin counts (-> start) and of the
             // fresh buckets each bin needs (-> nbase, relative); ONE global
@@ -481,7 +526,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                     // of a new reservation (a set out of buckets cannot
                     // happen within radix_need; such rows are dropped)
                     const unsigned need = xk - rem, take = need > kPoolBuckets ? need : kPoolBuckets;
-                    const unsigned nb = (ABL & 1) ? (unsigned)(((u64)tl.lo / kTile * 24u) % (a.max_buckets - 1024u))
+                    const unsigned nb = (ABL & 1) ? (unsigned)(((u64)t * 24u) % (a.max_buckets - 1024u))
                                                   : atomicAdd(a.nb, take);
                     if ((u64)nb + take <= a.max_buckets) {
                         s_nb2 = nb;
@@ -564,7 +609,8 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(4);
-        tl = ntl;
+        tseg = nseg_t;
+        tlo = ntlo;
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
             row[i] = nrow[i];
@@ -584,81 +630,114 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     }
 }
 
-// Bucket list by partition: count buckets per partition, exclusive scan
-// (k_scan_*), then place every bucket id at its partition's cursor.  Blocks
-// aggregate in LDS first when partitions are few (pass 1: 512).
+// Bucket list by partition: count buckets (and their runs) per partition,
+// exclusive scans (k_scan_*), then place every bucket id and its runs at its
+// partition's cursors.  Blocks aggregate in LDS first when partitions are
+// few (pass 1: 512).
 constexpr int kListPer = 4;
 constexpr int kListLds = 4096;
 
+__device__ __forceinline__ unsigned runs_of(unsigned fill) { return (fill + (1u << kRunLog) - 1) >> kRunLog; }
+
 // Buckets [0, *nb) of a pass, clamped to the set's capacity (the counter
 // passes it only when a pass ran out of buckets, which radix_need excludes).
-__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *nb, unsigned max_buckets,
-                                                 u64 *pcnt, int P) {
-    __shared__ unsigned c[kListLds];
+__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
+                                                 unsigned max_buckets, u64 *pcnt, u64 *rcnt, int P) {
+    __shared__ unsigned c[kListLds], cr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
     const bool lds = P <= kListLds;
     if (lds)
-        for (int i = threadIdx.x; i < P; i += 1024) c[i] = 0u;
+        for (int i = threadIdx.x; i < P; i += 1024) c[i] = cr[i] = 0u;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         const unsigned b = j < n ? bbin[j] : kNoBucket;
         if (b < (unsigned)P) {   // holes (unused pool ids) are kNoBucket
-            if (lds) atomicAdd(&c[b], 1u);
-            else atomicAdd(&pcnt[b], 1ull);
+            const unsigned nr = runs_of(bfill[j]);
+            if (lds) {
+                atomicAdd(&c[b], 1u);
+                atomicAdd(&cr[b], nr);
+            } else {
+                atomicAdd(&pcnt[b], 1ull);
+                atomicAdd(&rcnt[b], (u64)nr);
+            }
         }
     }
     if (!lds) return;
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += 1024)
-        if (c[i]) atomicAdd(&pcnt[i], (u64)c[i]);
+        if (c[i]) {
+            atomicAdd(&pcnt[i], (u64)c[i]);
+            atomicAdd(&rcnt[i], (u64)cr[i]);
+        }
 }
 
 __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, u64 *pcur, u64 *blist, int P) {
-    __shared__ unsigned c[kListLds];
-    __shared__ u64 cb[kListLds];
+                                                 unsigned max_buckets, int pbl, u64 *pcur, u64 *rcur, u64 *blist,
+                                                 u64 *runs, int P) {
+    __shared__ unsigned c[kListLds], cr[kListLds];
+    __shared__ u64 cb[kListLds], cbr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
+    // bucket j's runs: rows (j << pbl) + 64 k, count min(64, fill - 64 k)
+    auto put_runs = [&](u64 j, unsigned f, u64 at) {
+        for (unsigned k = 0; (k << kRunLog) < f; ++k) {
+            const unsigned cnt = f - (k << kRunLog) < (1u << kRunLog) ? f - (k << kRunLog) : (1u << kRunLog);
+            runs[at + k] = ((((u64)j << pbl) + ((u64)k << kRunLog)) << 7) | cnt;
+        }
+    };
     if (P > kListLds) {
 #pragma unroll
         for (int i = 0; i < kListPer; ++i) {
             const u64 j = base + (u64)i * 1024 + threadIdx.x;
             const unsigned b = j < n ? bbin[j] : kNoBucket;
-            if (b < (unsigned)P) blist[atomicAdd(&pcur[b], 1ull)] = (j << 32) | bfill[j];
+            if (b < (unsigned)P) {
+                const unsigned f = bfill[j];
+                blist[atomicAdd(&pcur[b], 1ull)] = (j << 32) | f;
+                put_runs(j, f, atomicAdd(&rcur[b], (u64)runs_of(f)));
+            }
         }
         return;
     }
-    for (int i = threadIdx.x; i < P; i += 1024) c[i] = 0u;
+    for (int i = threadIdx.x; i < P; i += 1024) c[i] = cr[i] = 0u;
     __syncthreads();
-    unsigned rk[kListPer], bn[kListPer];
+    unsigned rk[kListPer], rr[kListPer], bn[kListPer], fl[kListPer];
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         bn[i] = j < n ? bbin[j] : kNoBucket;
         if (bn[i] >= (unsigned)P) bn[i] = kNoBucket;
-        if (bn[i] != kNoBucket) rk[i] = atomicAdd(&c[bn[i]], 1u);
+        fl[i] = bn[i] != kNoBucket ? bfill[j] : 0u;
+        if (bn[i] != kNoBucket) {
+            rk[i] = atomicAdd(&c[bn[i]], 1u);
+            rr[i] = atomicAdd(&cr[bn[i]], runs_of(fl[i]));
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += 1024)
-        if (c[i]) cb[i] = atomicAdd(&pcur[i], (u64)c[i]);
+        if (c[i]) {
+            cb[i] = atomicAdd(&pcur[i], (u64)c[i]);
+            cbr[i] = atomicAdd(&rcur[i], (u64)cr[i]);
+        }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
-        if (bn[i] != kNoBucket) blist[cb[bn[i]] + rk[i]] = (j << 32) | bfill[j];
+        if (bn[i] == kNoBucket) continue;
+        blist[cb[bn[i]] + rk[i]] = (j << 32) | fl[i];
+        put_runs(j, fl[i], cbr[bn[i]] + rr[i]);
     }
 }
 
 // --------------------------------------------------------------- join
 struct JoinArgs {
     const void *r, *s;               // final-pass bucket rows
-    const u64 *r_list, *s_list;      // buckets by partition (bucket << 32 | fill), kFinalPbl rows each
-    const u64 *r_pstart, *s_pstart;  // P + 1 each
+    const u64 *r_runs, *s_runs;      // runs by partition (row << 7 | count)
+    const u64 *r_rstart, *s_rstart;  // P + 1 each
     int P;
     const unsigned *work_start;      // P + 1: S chunks per partition (0 if no R rows)
     const struct ItemDesc *desc;     // per work item (k_item_desc)
@@ -670,33 +749,32 @@ struct JoinArgs {
 };
 
 struct ItemDesc {
-    u64 s_lo, s_hi, r_lo, r_hi;      // bucket-list positions of the item's S chunk / the partition's R
+    u64 s_lo, s_hi, r_lo, r_hi;      // run positions of the item's S chunk / the partition's R
 };
 
 // One descriptor per work item, so the join reads its item with one
 // (scalar) load instead of the owner -> partition -> offsets chain.
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
-                                                   const u64 *s_pstart, const u64 *r_pstart, int P, unsigned chb,
+                                                   const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
                                                    ItemDesc *desc) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
     if (w >= work_start[P]) return;
     const int p = (int)work_owner[w];
     const unsigned c = w - work_start[p];
     ItemDesc d;
-    d.s_lo = s_pstart[p] + (u64)c * chb;
-    const u64 e = s_pstart[p + 1];
-    d.s_hi = d.s_lo + chb < e ? d.s_lo + chb : e;
-    d.r_lo = r_pstart[p];
-    d.r_hi = r_pstart[p + 1];
+    d.s_lo = s_rstart[p] + (u64)c * chr;
+    const u64 e = s_rstart[p + 1];
+    d.s_hi = d.s_lo + chr < e ? d.s_lo + chr : e;
+    d.r_lo = r_rstart[p];
+    d.r_hi = r_rstart[p + 1];
     desc[w] = d;
 }
 
 // A persistent workgroup of NT threads walks work items w = wg, wg + grid, ...
-// Work item = (partition, chunk of up to kJoinSub * NT * SI / PB S buckets):
-// build the partition's R buckets into a 2^TSL-slot LDS table (rounds of
-// RCAP / PB buckets for oversized partitions), then probe the chunk in
-// sub-chunks of NT * SI / PB buckets.  Requires PB | RCAP
-// and PB | NT * SI (host-checked).
+// Work item = (partition, chunk of up to kJoinSub * NT * SI / 64 S runs):
+// build the partition's R runs into a 2^TSL-slot LDS table (rounds of
+// RCAP / 64 runs for oversized partitions), then probe the chunk in
+// sub-chunks of NT * SI / 64 runs.
 // ABL (diagnostics only, micro/join_micro.hip; the product uses 0) switches
 // phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build,
 // 16 probe reads the first slot only.
@@ -711,10 +789,10 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     constexpr int RCAP = TS * 5 / 8;          // build rows per round (load factor <= 0.625)
     constexpr int RI = RCAP / NT;             // build rows per thread per round
     constexpr int SUBR = NT * SI;             // rows per sub-chunk
-    constexpr unsigned rb = (unsigned)RCAP >> kFinalPbl;     // buckets per build round
-    constexpr unsigned subb = (unsigned)SUBR >> kFinalPbl;   // buckets per sub-chunk
-    constexpr unsigned chb = (unsigned)kJoinSub * subb;      // buckets per work item
-    static_assert((rb << kFinalPbl) == RCAP && (subb << kFinalPbl) == SUBR, "bucket size must divide rounds");
+    constexpr unsigned rb = (unsigned)RCAP >> kRunLog;       // runs per build round
+    constexpr unsigned subb = (unsigned)SUBR >> kRunLog;     // runs per sub-chunk
+    constexpr unsigned chb = (unsigned)kJoinSub * subb;      // runs per work item
+    static_assert((rb << kRunLog) == RCAP && (subb << kRunLog) == SUBR, "rounds must be whole runs");
     // wide: EMPTY key INT64_MIN (rows with that key take the null path);
     // narrow: the all-ones word (row ids < 2^31 never produce it)
     constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
@@ -734,19 +812,18 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
 
-    // Row slot i of thread t is row (t % PB) of bucket lo + i * G + t / PB
-    // (G = NT / PB buckets per slot): a wave's 64 lanes share the bucket, so
-    // list entries are wave-uniform (scalar loads into SGPRs) and can be
-    // fetched one item ahead without costing VGPRs.
-    constexpr unsigned G = NT >> kFinalPbl;
-    static_assert((G << kFinalPbl) == NT, "workgroup must span whole buckets");
-    const unsigned hb = __builtin_amdgcn_readfirstlane(threadIdx.x >> kFinalPbl);
-    const unsigned off = threadIdx.x & ((1u << kFinalPbl) - 1u);
-    // list entries (bucket << 32 | fill; 0 = none) of positions [lo, min(lo + n*G, hi))
+    // Row slot i of wave v is run lo + i * NW + v, lane l its row l: the
+    // run entry is wave-uniform (scalar loads into SGPRs) and can be
+    // fetched one item ahead without costing VGPRs; a partly filled bucket
+    // idles at most the tail of its last run.
+    constexpr unsigned G = NT >> kRunLog;
+    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
+    const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
+    // run entries (row << 7 | count; 0 = none) of positions [lo, min(lo + n*G, hi))
     auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-            const u64 li = lo + (u64)i * G + hb;
+            const u64 li = lo + (u64)i * G + wv0;
             e[i] = li < hi ? list[li] : 0ull;
         }
     };
@@ -754,8 +831,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
         unsigned ok = 0;
 #pragma unroll
         for (int i = 0; i < n; ++i) {
-            if (off < (unsigned)e[i]) {
-                v[i] = rows[((e[i] >> 32) << kFinalPbl) + off];
+            if (off < (unsigned)(e[i] & 127u)) {
+                v[i] = rows[(e[i] >> 7) + off];
                 ok |= 1u << i;
             } else {
                 v[i] = R::zero();
@@ -767,15 +844,15 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
     u64 er[RI], es[SI];
     ItemDesc it = a.desc[w];
-    ents(a.r_list, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
-    ents(a.s_list, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    ents(a.r_runs, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
+    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
     ItemDesc nx = a.desc[w + gridDim.x < total ? w + gridDim.x : w];
     auto load_r = [&](u64 r0) {
-        ents(a.r_list, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
+        ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
         return rows_of(rrows, er, rv_, RI);
     };
     auto load_s = [&](u64 s0) {
-        ents(a.s_list, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
+        ents(a.s_runs, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
         return rows_of(srows, es, sv_, SI);
     };
     while (true) {
@@ -790,8 +867,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
         u64 ner[RI], nes[SI];
         ItemDesc nnx = nx;
         if (more) {
-            ents(a.r_list, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
-            ents(a.s_list, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+            ents(a.r_runs, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
+            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
             if (w + 2 * gridDim.x < total) nnx = a.desc[w + 2 * gridDim.x];
         }
 
@@ -957,7 +1034,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                             run += v[k];
                         }
                         if (lane == 63 && x)
-                            s_base = (ABL & 1) ? (u64)w * chb << kFinalPbl : atomicAdd(a.counter, (u64)x);
+                            s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, (u64)x);
                     }
                     __syncthreads();
 #pragma unroll
@@ -978,7 +1055,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                 if constexpr (!WRITE) {
                     if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
                 } else if (tot) {
-                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kFinalPbl : atomicAdd(a.counter, tot);
+                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, tot);
                     __syncthreads();
                     u64 pos = s_base + pre;
 #pragma unroll
@@ -1039,9 +1116,9 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                         for (int i = 0; i < SI; ++i) {
                             if (!(((sok >> i) & 1u) && R::key(sv_[i]) == kEmptyKey64)) continue;
                             for (u64 li = it.r_lo; li < it.r_hi; ++li) {
-                                const u64 le = a.r_list[li];
-                                for (unsigned o = 0; o < (unsigned)le; ++o) {
-                                    const T rr = rrows[((le >> 32) << kFinalPbl) + o];
+                                const u64 le = a.r_runs[li];
+                                for (unsigned o = 0; o < (unsigned)(le & 127u); ++o) {
+                                    const T rr = rrows[(le >> 7) + o];
                                     if (R::key(rr) != kEmptyKey64) continue;
                                     if (pos < (u64)a.cap) {
                                         orr[pos] = (PT)R::pay(rr);
@@ -1168,8 +1245,9 @@ RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
 }
 
 unsigned long long radix_tiles(long long n, int max_nseg) {
-    // bucketed tiles: kTile / PB buckets each, <= one partial tile per segment
-    return (u64)(n > 0 ? n : 1) / kTile * 2 + (u64)max_nseg + 2;
+    // bucketed tiles: kTile / 64 runs each, <= one partial tile per segment;
+    // every run holds >= 1 row, so runs <= n (the bound is loose but small)
+    return (u64)(n > 0 ? n : 1) / (kTile >> kRunLog) + (u64)max_nseg + 2;
 }
 
 size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
@@ -1183,10 +1261,10 @@ hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, uns
 
 size_t exclusive_scan_sums(unsigned long long len) { return (size_t)(len / kScanBlock + 2); }
 
-unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_buckets) {
+unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs) {
     const JoinVariant jv = join_variant();
-    const u64 chb = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kFinalPbl);
-    return s_buckets / chb + (1ull << pl.total_bits) + 2;
+    const u64 chr = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kRunLog);
+    return s_runs / chr + (1ull << pl.total_bits) + 2;
 }
 
 // Partition one relation into the plan's 2^total_bits partitions: bucket
@@ -1198,7 +1276,6 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
     int nseg = 1;
     int shift = 64;
     const BucketSet *prev = nullptr;
-    int prev_pbl = 0;
     const unsigned grid = pass_grid(n > 0 ? n : 1);
     for (int pass = 0; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
@@ -1209,10 +1286,12 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         a.n = n;
         a.cols_aligned = ((((uintptr_t)src.key) | ((uintptr_t)src.pay)) & 15) == 0;
         a.in_rows = prev ? prev->rows : nullptr;
-        a.in_list = prev ? prev->blist : nullptr;
-        a.in_pstart = prev ? prev->pstart : nullptr;
+        a.in_runs = prev ? prev->runs : nullptr;
+        a.in_rstart = prev ? prev->rstart : nullptr;
+        a.in_max_rows = prev ? prev->max_rows : 0;
+        a.in_max_runs = prev ? prev->max_runs : 0;
         a.tile_start = ws.tile_start;
-        a.tile_owner = ws.tile_owner;
+        a.tdesc = nullptr;
         a.nseg = nseg;
         a.out_rows = dst.rows;
         a.bbin = dst.bbin;
@@ -1230,10 +1309,15 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         hipError_t e = hipMemsetAsync(ws.nb, 0, sizeof(unsigned), st);
         if (e != hipSuccess) return e;
         if (prev) {
-            // tiles of kTile / PB buckets per segment, and tile -> segment
-            if (prev_pbl != kPassPbl) return hipErrorInvalidValue;   // pass inputs are kPassPbl buckets
-            chunk_map(prev->pstart, nullptr, nseg, (unsigned)(kTile >> kPassPbl), ws.tile_start, ws.tile_owner, ws.pcur,
+            // tiles of kTile / 64 runs per segment, tile -> segment, and one
+            // descriptor per tile
+            chunk_map(prev->rstart, nullptr, nseg, (unsigned)(kTile >> kRunLog), ws.tile_start, ws.tile_owner, ws.pcur,
                       ws.scan_sums, st);
+            const u64 tb = radix_tiles((long long)n, nseg);
+            hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, st, (const unsigned *)ws.tile_start,
+                               (const unsigned *)ws.tile_owner, (const u64 *)prev->rstart, nseg, (unsigned)tb,
+                               (TileDesc *)ws.tdesc);
+            a.tdesc = (const TileDesc *)ws.tdesc;
         }
         if (n > 0) {
 #define HJ_PASS(W, FORM) hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
@@ -1249,30 +1333,38 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
             }
 #undef HJ_PASS
         }
-        // list the buckets by partition: pstart = scan of per-partition counts
+        // list the buckets and their runs by partition: pstart / rstart =
+        // scans of per-partition counts
         const u64 P = (u64)nseg << fb;
         e = hipMemsetAsync(dst.pstart, 0, (P + 1) * sizeof(u64), st);
         if (e != hipSuccess) return e;
+        e = hipMemsetAsync(dst.rstart, 0, (P + 1) * sizeof(u64), st);
+        if (e != hipSuccess) return e;
+        // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
+        if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
         const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
-        hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin, (const unsigned *)ws.nb,
-                           a.max_buckets, dst.pstart, (int)P);
+        hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, dst.pstart, dst.rstart,
+                           (int)P);
         scan_u64(dst.pstart, P + 1, ws.scan_sums, st);
+        scan_u64(dst.rstart, P + 1, ws.scan_sums, st);
         e = hipMemcpyAsync(ws.pcur, dst.pstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return e;
+        e = hipMemcpyAsync(ws.rcur, dst.rstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, ws.pcur, dst.blist,
-                           (int)P);
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass], ws.pcur,
+                           ws.rcur, dst.blist, dst.runs, (int)P);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         prev = &dst;
-        prev_pbl = pl.pbl[pass];
         nseg = (int)P;
     }
     return hipSuccess;
 }
 
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
-                      unsigned s_buckets, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
+                      unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
@@ -1281,25 +1373,25 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     // persistent grid: as many workgroups as fit at once (LDS-limited)
     const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
     const unsigned pg = (unsigned)(per_cu * cu_count());
-    // S buckets per work item: at least kJoinSub sub-chunks, more when S is
+    // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
     // long as ~16 items per workgroup remain for balance
-    const unsigned subb = (unsigned)((jv.nt * kJoinItems) >> kFinalPbl);
+    const unsigned subb = (unsigned)((jv.nt * kJoinItems) >> kRunLog);
     u64 chb = (u64)kJoinSub * subb;
-    const u64 want = (u64)s_buckets / (16ull * pg);
+    const u64 want = (u64)s_runs / (16ull * pg);
     if (want > chb) chb = (want + subb - 1) / subb * subb;
-    chunk_map(s.pstart, r.pstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
-    const unsigned items = (unsigned)((u64)s_buckets / chb + (u64)P + 1);
+    chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
-                       (const unsigned *)work_owner, (const u64 *)s.pstart, (const u64 *)r.pstart, P, (unsigned)chb,
+                       (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
                        (ItemDesc *)desc);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
-    a.r_list = r.blist;
-    a.s_list = s.blist;
-    a.r_pstart = r.pstart;
-    a.s_pstart = s.pstart;
+    a.r_runs = r.runs;
+    a.s_runs = s.runs;
+    a.r_rstart = r.rstart;
+    a.s_rstart = s.rstart;
     a.P = P;
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;

@@ -41,8 +41,11 @@ BucketSet make_set(RadixNeed nd, int P) {
     b.bfill = dalloc<unsigned>(nd.buckets);
     b.blist = dalloc<u64>(nd.buckets);
     b.pstart = dalloc<u64>((u64)P + 1);
+    b.rstart = dalloc<u64>((u64)P + 1);
     b.max_buckets = (unsigned)nd.buckets;
     b.max_rows = nd.rows;
+    b.max_runs = (nd.rows >> kRunLog) + nd.buckets;
+    b.runs = dalloc<u64>(b.max_runs);
     return b;
 }
 
@@ -57,8 +60,10 @@ int main() {
     ws.tmp = make_set(radix_need((long long)n, pl, false), P);
     ws.nb = dalloc<unsigned>(4);
     ws.pcur = dalloc<u64>(P + 1);
+    ws.rcur = dalloc<u64>(P + 1);
     ws.tile_start = dalloc<unsigned>(P + 1);
     ws.tile_owner = dalloc<unsigned>(radix_tiles((long long)n, P));
+    ws.tdesc = dalloc<char>(radix_tiles((long long)n, P) * 16);
     ws.scan_sums = dalloc<u64>(P / 8192 + 2);
     const RadixNeed nd = radix_need((long long)n, pl, true);
     BucketSet rs = make_set(nd, P), ss = make_set(nd, P);
@@ -97,8 +102,8 @@ int main() {
         printf("%s: buckets %llu rows %llu partial %llu (%.2f/partition) max buckets %llu max rows %llu  >8 bk %.1f%%  >10 bk %.1f%%\n",
                side ? "S" : "R", ps[P], rows, part, (double)part / P, maxb, maxrows, 100.0 * over8 / P, 100.0 * over10 / P);
     }
-    unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_buckets));
-    void *desc = dalloc<char>(radix_join_items(pl, ss.max_buckets) * radix_item_desc_bytes());
+    unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_runs));
+    void *desc = dalloc<char>(radix_join_items(pl, ss.max_runs) * radix_item_desc_bytes());
     u64 *out_r = dalloc<u64>(n + (1 << 20)), *out_s = dalloc<u64>(n + (1 << 20)), *cnt = dalloc<u64>(8),
         *dup = dalloc<u64>(8);
     hipEvent_t e0, e1;
@@ -124,12 +129,12 @@ int main() {
         printf("%-34s %7.3f ms  %7.1f GB/s  M=%llu\n", name, ms, (3.0 * n * 16) / ms / 1e6, m);
     };
     run("radix_join (product)", [&] {
-        CK(radix_join(true, pl, ws, rs, ss, ss.max_buckets, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0));
+        CK(radix_join(true, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0));
     });
     // work map of the product call stays in `work`
     JoinArgs a;
-    a.r = rs.rows; a.s = ss.rows; a.r_list = rs.blist; a.s_list = ss.blist; a.r_pstart = rs.pstart;
-    a.s_pstart = ss.pstart; a.P = P; a.work_start = work; a.desc = (const ItemDesc *)desc;
+    a.r = rs.rows; a.s = ss.rows; a.r_runs = rs.runs; a.s_runs = ss.runs; a.r_rstart = rs.rstart;
+    a.s_rstart = ss.rstart; a.P = P; a.work_start = work; a.desc = (const ItemDesc *)desc;
     a.out_r = out_r; a.out_s = out_s; a.cap = (long long)n; a.counter = cnt; a.dup_flag = dup;
     const int cus = cu_count();
 #define J(TSL, NT, PER_CU, WR, ABL, NAME)                                                                  \

@@ -106,5 +106,128 @@ int main() {
             CK(hipFree(prof));
         }
     }
+    // ---- a real second pass: the bucketed output of a 512-bin first pass
+    // (512-row buckets, listed as runs) partitioned by the next 8 bits into
+    // 256-row buckets, as radix_partition's pass 2 at |R| = 2^28
+    {
+        RadixPlan p1{};
+        p1.passes = 1;
+        p1.bits[0] = 9;
+        p1.pbl[0] = kPassPbl;
+        p1.total_bits = 9;
+        const int P1 = 512;
+        RadixNeed nd = radix_need((long long)n, p1, true);
+        BucketSet b1;
+        CK(hipMalloc(&b1.rows, nd.rows * 16));
+        CK(hipMalloc(&b1.bbin, nd.buckets * 4));
+        CK(hipMalloc(&b1.bfill, nd.buckets * 4));
+        CK(hipMalloc(&b1.blist, nd.buckets * 8));
+        CK(hipMalloc(&b1.pstart, (P1 + 1) * 8));
+        CK(hipMalloc(&b1.rstart, (P1 + 1) * 8));
+        b1.max_buckets = (unsigned)nd.buckets;
+        b1.max_rows = nd.rows;
+        b1.max_runs = (nd.rows >> kRunLog) + nd.buckets;
+        CK(hipMalloc(&b1.runs, b1.max_runs * 8));
+        const int P2 = P1 << 8;
+        RadixWork ws{};
+        CK(hipMalloc(&ws.nb, 64));
+        CK(hipMalloc(&ws.pcur, (P2 + 1) * 8));
+        CK(hipMalloc(&ws.rcur, (P2 + 1) * 8));
+        CK(hipMalloc(&ws.tile_start, (P2 + 1) * 4));
+        CK(hipMalloc(&ws.tile_owner, radix_tiles((long long)n, P2) * 4));
+        CK(hipMalloc(&ws.tdesc, radix_tiles((long long)n, P2) * 16));
+        CK(hipMalloc(&ws.scan_sums, (P2 / 8192 + 2) * 8));
+        SrcDev src{};
+        src.form = kPacked64;
+        src.key = in;
+        src.n = (long long)n;
+        CK(radix_partition(src, true, p1, ws, b1, 0));
+        chunk_map(b1.rstart, nullptr, P1, (unsigned)(kTile >> kRunLog), ws.tile_start, ws.tile_owner, ws.pcur,
+                  ws.scan_sums, 0);
+        {
+            const u64 tb = radix_tiles((long long)n, P1);
+            hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, 0, (const unsigned *)ws.tile_start,
+                               (const unsigned *)ws.tile_owner, (const u64 *)b1.rstart, P1, (unsigned)tb,
+                               (TileDesc *)ws.tdesc);
+        }
+        CK(hipDeviceSynchronize());
+        unsigned ntiles = 0;
+        u64 nruns = 0, nbk = 0;
+        CK(hipMemcpy(&ntiles, ws.tile_start + P1, 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&nruns, b1.rstart + P1, 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(&nbk, b1.pstart + P1, 8, hipMemcpyDeviceToHost));
+        printf("pass-1 set: %llu buckets, %llu runs (%.3f x n/64), %u pass-2 tiles (%.3f x n/4096)\n", nbk, nruns,
+               nruns / (double)(n >> 6), ntiles, ntiles / (double)(n >> 12));
+        PassArgs b{};
+        b.n = n;
+        b.in_rows = b1.rows;
+        b.in_runs = b1.runs;
+        b.in_rstart = b1.rstart;
+        b.in_max_rows = b1.max_rows;
+        b.in_max_runs = b1.max_runs;
+        b.tile_start = ws.tile_start;
+        b.tdesc = (const TileDesc *)ws.tdesc;
+        b.nseg = P1;
+        b.out_rows = out;
+        b.bbin = bbin;
+        b.bfill = bfill;
+        b.nb = nb;
+        b.max_buckets = (unsigned)maxb;
+        b.out_pbl = kFinalPbl;
+        b.fbits = 8;
+        b.shift = 64 - 17;
+        {
+            // correctness: every row must land in the pass-2 output exactly once
+            CK(hipMemset(nb, 0, 4));
+            hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b);
+            CK(hipDeviceSynchronize());
+            unsigned nbh = 0;
+            CK(hipMemcpy(&nbh, nb, 4, hipMemcpyDeviceToHost));
+            std::vector<unsigned> bb(nbh), bf(nbh);
+            CK(hipMemcpy(bb.data(), bbin, nbh * 4ull, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(bf.data(), bfill, nbh * 4ull, hipMemcpyDeviceToHost));
+            u64 rows = 0, used = 0;
+            for (unsigned j = 0; j < nbh; ++j)
+                if (bb[j] != kNoBucket) {
+                    rows += bf[j];
+                    ++used;
+                }
+            std::vector<ulonglong2> td(ntiles);
+            CK(hipMemcpy(td.data(), ws.tdesc, ntiles * 16ull, hipMemcpyDeviceToHost));
+            u64 druns = 0;
+            for (unsigned t = 0; t < ntiles; ++t) druns += (unsigned)td[t].y;
+            printf("pass-2 check: %u bucket ids, %llu used, %llu rows out of %llu (%s); descriptors cover %llu runs of %llu\n",
+                   nbh, used, rows, n, rows == n ? "ok" : "MISMATCH", druns, nruns);
+        }
+        run("pass 2 (F256 PB256, runs) k_pass", [&] { hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b); });
+#define P2X(ABL, TXT) run("pass 2 " TXT, [&] { hipLaunchKernelGGL((k_pass<true, kBucketed, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b); })
+        P2X(1, "no bucket atomic");
+        P2X(2, "synthetic rows");
+        P2X(4, "no row stores");
+        P2X(6, "synthetic rows, no stores");
+#undef P2X
+        b.out_pbl = kPassPbl;
+        run("pass 2 with 512-row output buckets", [&] { hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b); });
+        b.out_pbl = kFinalPbl;
+        u64 *prof;
+        CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
+        CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
+        b.prof = prof;
+        CK(hipMemset(nb, 0, 4));
+        hipLaunchKernelGGL((k_pass<true, kBucketed, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b);
+        CK(hipDeviceSynchronize());
+        std::vector<u64> h(grid * 8);
+        CK(hipMemcpy(h.data(), prof, h.size() * sizeof(u64), hipMemcpyDeviceToHost));
+        const char *names[5] = {"load wait + hash + LDS count", "scan + bucket atomic", "LDS scatter",
+                                "next loads issued + stores + tails", "new tails + bookkeeping"};
+        double m[5], tot = 0;
+        for (int k = 0; k < 5; ++k) {
+            double acc = 0;
+            for (unsigned g = 0; g < grid; ++g) acc += (double)h[g * 8 + k];
+            m[k] = acc / grid;
+            tot += m[k];
+        }
+        for (int k = 0; k < 5; ++k) printf("  pass 2 phase %-38s %10.0f cycles  %5.1f %%\n", names[k], m[k], 100.0 * m[k] / tot);
+    }
     return 0;
 }
