@@ -114,7 +114,7 @@ struct hj_ctx {
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
-    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, work_start, work_desc, scan_sums;
+    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, wstart, work_start, work_desc, scan_sums;
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
@@ -247,6 +247,7 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     HJ_TRY(ensure_buf(c->tile_start, (P + 1) * 4));
     HJ_TRY(ensure_buf(c->tile_owner, (size_t)hj::radix_tiles(n, (int)P) * 4));
     HJ_TRY(ensure_buf(c->tdesc, (size_t)hj::radix_tiles(n, (int)P) * 16));
+    HJ_TRY(ensure_buf(c->wstart, 1025 * 4));
     // work map: P + 1 chunk starts, then the item -> partition owner list
     const size_t items = (size_t)hj::radix_join_items(pl, fin.max_runs);
     HJ_TRY(ensure_buf(c->work_start, (P + 1 + items) * 4));
@@ -264,6 +265,7 @@ hj::RadixWork radix_work(hj_ctx *c) {
     w.tile_start = (unsigned *)c->tile_start.p;
     w.tile_owner = (unsigned *)c->tile_owner.p;
     w.tdesc = c->tdesc.p;
+    w.wstart = (unsigned *)c->wstart.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
     return w;
 }
@@ -806,7 +808,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart, &sb->runs, &sb->rstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->work_start, &c->work_desc, &c->scan_sums,
+    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums,
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums})
         free_buf(*b);
     if (c->ev_ready)

@@ -119,6 +119,7 @@ struct RadixWork {                 // scratch shared by the partition passes
     unsigned *tile_start;          // >= P + 1
     unsigned *tile_owner;          // >= radix_tiles(n, P)
     void *tdesc;                   // >= radix_tiles(n, P) * 16 B: bucketed-pass tile descriptors
+    unsigned *wstart;              // >= 1025: per-workgroup bucket id ranges of a pass
     unsigned long long *scan_sums; // >= P / 8192 + 2
 };
 

@@ -12,7 +12,7 @@
 //                  8192-row tiles; it counting-sorts each tile by bin in LDS
 //                  and appends every bin's run to the workgroup's current
 //                  bucket for that bin (2^pbl rows; a full bucket is replaced
-//                  by fresh ones from one global atomic counter).  The input
+//                  by fresh ids from the workgroup's own id range).  The input
 //                  is read ONCE: no histogram pass and no global scan
 //                  (profiles/r01_micro_bucket_pass.txt: 2.27 ms per 2^28-row
 //                  pass vs 3.3 ms for histogram + exact-offset scatter).
@@ -53,10 +53,6 @@ constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
 constexpr int kPassPbl = 9;        // 512-row buckets for intermediate passes
 constexpr int kFinalPbl = 8;       // 256-row buckets for the join's input (less slack)
-#ifndef HJ_POOL_BUCKETS
-#define HJ_POOL_BUCKETS 64
-#endif
-constexpr unsigned kPoolBuckets = HJ_POOL_BUCKETS;   // bucket ids a pass workgroup reserves per global atomic
 
 __device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
 
@@ -213,6 +209,7 @@ struct PassArgs {
     // output set
     void *out_rows;
     unsigned *bbin, *bfill, *nb;
+    const unsigned *wstart;      // G + 1: workgroup w's bucket ids are [wstart[w], wstart[w + 1]) (k_id_plan)
     unsigned max_buckets;
     int out_pbl;
     int shift;                   // bin = (hash >> shift) & (F - 1)
@@ -285,10 +282,9 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ unsigned short sb[kTile];
     __shared__ __attribute__((aligned(16))) unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan],
         nbase[kMaxFan];
-    // the tile's fresh buckets: s_nrem from s_nb (the pool's rest), then
-    // from s_nb2 (a refill); kNoBucket when the set is exhausted
-    __shared__ unsigned s_nb, s_nrem, s_nb2;
-    __shared__ unsigned s_hole[2];
+    // the tile's fresh buckets: ids s_nb, s_nb + 1, ... (below s_nend)
+    __shared__ unsigned s_nb, s_nend;
+    __shared__ unsigned s_hole;
     const unsigned F = 1u << a.fbits;
     const unsigned PB = 1u << a.out_pbl;
     const unsigned T_ = pass_tiles<FORM>(a);
@@ -301,13 +297,14 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         fill[b] = PB;   // no open bucket (and no tail: PB is a whole number of lines)
     }
     // the tile's x-th fresh bucket
-    auto fresh = [&](unsigned x) -> unsigned {
-        return x < s_nrem ? s_nb + x : (s_nb2 == kNoBucket ? kNoBucket : s_nb2 + (x - s_nrem));
-    };
-    // fresh buckets are taken from a per-workgroup pool of kPoolBuckets ids
-    // (wave 0, lane 63): one returning global atomic per refill instead of
-    // one per tile, which stalled the workgroup at every tile's scan
-    unsigned pool_lo = 0u, pool_hi = 0u;
+    auto fresh = [&](unsigned x) -> unsigned { return s_nb + x < s_nend ? s_nb + x : kNoBucket; };
+    // fresh bucket ids come from the workgroup's own range (k_id_plan
+    // sizes it for the worst case of its tiles): no global atomic.  (A
+    // shared counter, even one returning atomic per 64 ids, cost 0.25-0.3 ms
+    // per 2^28-row pass: waiting for its result also waited for the next
+    // tile's loads, profiles/r01_micro_pass2.txt "no bucket atomic".)
+    const unsigned id_end = a.wstart[blockIdx.x + 1];
+    unsigned id_next = a.wstart[blockIdx.x];
     // row slot of position p (>= the line start of fill[b]) of bin b's run
     // in the current tile: the open bucket, then the tile's fresh buckets
     auto slot = [&](unsigned b, unsigned p) -> u64 {
@@ -470,9 +467,8 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         if (threadIdx.x < 64) {
             // wave 0: exclusive scans of the bin counts (-> start) and of the
-            // fresh buckets each bin needs (-> nbase, relative); ONE global
-            // atomic reserves the tile's buckets (a counter hit once per bin
-            // allocation serialised ~1M atomics per 2^28-row pass)
+            // fresh buckets each bin needs (-> nbase, relative); the tile's
+            // fresh buckets are the next ids of the workgroup's range
             const int lane = threadIdx.x;
             // (8 bins per lane moved as two 16-B LDS accesses per array:
             // wave 0 alone is on the critical path here)
@@ -515,27 +511,9 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 ((uint4 *)nbase)[lane * 2 + 1] = make_uint4(nv[4], nv[5], nv[6], nv[7]);
             }
             if (lane == 63) {
-                const unsigned rem = pool_hi - pool_lo;
-                s_nb = pool_lo;
-                s_nrem = xk < rem ? xk : rem;
-                s_nb2 = kNoBucket;
-                if (xk <= rem) {
-                    pool_lo += xk;
-                } else {
-                    // refill: the tile takes the pool's rest, then the start
-                    // of a new reservation (a set out of buckets cannot
-                    // happen within radix_need; such rows are dropped)
-                    const unsigned need = xk - rem, take = need > kPoolBuckets ? need : kPoolBuckets;
-                    const unsigned nb = (ABL & 1) ? (unsigned)(((u64)t * 24u) % (a.max_buckets - 1024u))
-                                                  : atomicAdd(a.nb, take);
-                    if ((u64)nb + take <= a.max_buckets) {
-                        s_nb2 = nb;
-                        pool_lo = nb + need;
-                        pool_hi = nb + take;
-                    } else {
-                        pool_lo = pool_hi = 0u;
-                    }
-                }
+                s_nb = id_next;
+                s_nend = id_end;
+                id_next = xk < id_end - id_next ? id_next + xk : id_end;
             }
         }
         __syncthreads();
@@ -618,16 +596,38 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
     }
     close_all();
-    if (threadIdx.x == 63) {
-        s_hole[0] = pool_lo;
-        s_hole[1] = pool_hi;
-    }
+    // ids of the range left unused are holes for the bucket listing
+    if (threadIdx.x == 63) s_hole = id_next;
     __syncthreads();
-    for (unsigned i = s_hole[0] + threadIdx.x; i < s_hole[1]; i += kPassThreads) a.bbin[i] = kNoBucket;
+    for (unsigned i = s_hole + threadIdx.x; i < id_end; i += kPassThreads) a.bbin[i] = kNoBucket;
     if constexpr ((ABL & 8) != 0) {
         if (threadIdx.x == 0 && a.prof)
             for (int k = 0; k < 6; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
     }
+}
+
+// Bucket id ranges of a pass's workgroups (one block, G <= 1024): workgroup
+// w gets ceil(rows_w / PB) + segs_w * F + 1 ids, rows_w <= its tiles * kTile
+// and segs_w the segments its tiles span.  A bin's rows of one segment run
+// fill ceil(r / PB) <= r / PB + 1 buckets (a bucket is only taken for rows),
+// so the range never runs out.  *nb = the ids handed out (listing bound).
+__global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, unsigned G, unsigned *wstart) {
+    __shared__ u64 wsum[16];
+    const unsigned w = threadIdx.x;
+    const unsigned T_ = bucketed ? a.tile_start[a.nseg] : (unsigned)((a.n + kTile - 1) / kTile);
+    u64 q = 0;
+    if (w < G) {
+        const unsigned t0 = (unsigned)((u64)w * T_ / G), t1 = (unsigned)((u64)(w + 1) * T_ / G);
+        if (t1 > t0) {
+            const u64 segs = bucketed ? (u64)(a.tdesc[t1 - 1].seg - a.tdesc[t0].seg + 1) : 1ull;
+            const u64 PB = 1ull << a.out_pbl;
+            q = ((u64)(t1 - t0) * kTile + PB - 1) / PB + segs * (1ull << a.fbits) + 1;
+        }
+    }
+    u64 tot;
+    const u64 pre = block_excl_scan<1024>(q, wsum, &tot);
+    if (w <= G) wstart[w] = (unsigned)(pre < a.max_buckets ? pre : a.max_buckets);
+    if (w == G) *a.nb = (unsigned)(tot < a.max_buckets ? tot : a.max_buckets);
 }
 
 // Bucket list by partition: count buckets (and their runs) per partition,
@@ -1227,14 +1227,17 @@ RadixPlan radix_plan(long long n_build, int force_bits) {
 RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
     RadixNeed need{1, 1};
     const u64 rows = n > 0 ? (u64)n : 1;
-    u64 nseg = 1;
+    u64 nseg = 1, prev_b = 0;
     for (int i = 0; i < pl.passes; ++i) {
         const bool to_final = ((pl.passes - 1 - i) % 2) == 0;
         const u64 F = 1ull << pl.bits[i];
-        // every bucket holds >= 1 row, so never more than `rows` buckets
-        const u64 open = ((u64)pass_grid(rows) + nseg + 1) * F;
-        const u64 holes = (u64)pass_grid(rows) * kPoolBuckets;   // each workgroup's unused pool rest
-        const u64 b = (rows >> pl.pbl[i]) + (open < rows ? open : rows) + holes + 1;
+        // k_id_plan's ranges: sum over workgroups of ceil(tiles_w * kTile /
+        // PB) + segs_w * F + 1, with sum segs_w <= nseg + G; tiles of a
+        // bucketed pass <= runs / 64 + nseg, runs <= rows / 64 + buckets_in
+        const u64 G = pass_grid(rows);
+        const u64 tiles = i == 0 ? (rows + kTile - 1) / kTile : (rows / 64 + prev_b) / 64 + nseg + 1;
+        const u64 b = (tiles * kTile >> pl.pbl[i]) + G + (nseg + G) * F + G + 1;
+        prev_b = b;
         if (to_final == final_set) {
             if (b > need.buckets) need.buckets = b;
             if ((b << pl.pbl[i]) > need.rows) need.rows = b << pl.pbl[i];
@@ -1306,8 +1309,7 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
         a.out_pbl = pl.pbl[pass];
         a.shift = shift;
         a.fbits = fb;
-        hipError_t e = hipMemsetAsync(ws.nb, 0, sizeof(unsigned), st);
-        if (e != hipSuccess) return e;
+        hipError_t e = hipSuccess;
         if (prev) {
             // tiles of kTile / 64 runs per segment, tile -> segment, and one
             // descriptor per tile
@@ -1319,6 +1321,9 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
                                (TileDesc *)ws.tdesc);
             a.tdesc = (const TileDesc *)ws.tdesc;
         }
+        a.wstart = ws.wstart;
+        if (grid > 1024) return hipErrorInvalidValue;   // k_id_plan: one block
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, st, a, prev != nullptr, grid, ws.wstart);
         if (n > 0) {
 #define HJ_PASS(W, FORM) hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
             if (prev) {

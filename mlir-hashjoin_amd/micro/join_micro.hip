@@ -64,6 +64,7 @@ int main() {
     ws.tile_start = dalloc<unsigned>(P + 1);
     ws.tile_owner = dalloc<unsigned>(radix_tiles((long long)n, P));
     ws.tdesc = dalloc<char>(radix_tiles((long long)n, P) * 16);
+    ws.wstart = dalloc<unsigned>(1025);
     ws.scan_sums = dalloc<u64>(P / 8192 + 2);
     const RadixNeed nd = radix_need((long long)n, pl, true);
     BucketSet rs = make_set(nd, P), ss = make_set(nd, P);

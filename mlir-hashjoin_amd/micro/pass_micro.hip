@@ -45,6 +45,9 @@ int main() {
     a.bfill = bfill;
     a.nb = nb;
     a.max_buckets = (unsigned)maxb;
+    unsigned *wst;
+    CK(hipMalloc(&wst, 1025 * 4));
+    a.wstart = wst;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -72,11 +75,16 @@ int main() {
             a.out_pbl = pbl;
             char nm[64];
             snprintf(nm, sizeof nm, "F%d PB%d k_pass", 1 << fb, 1 << pbl);
-            run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow>), dim3(grid), dim3(kPassThreads), 0, 0, a); });
+            run(nm, [&] {
+                hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);
+                hipLaunchKernelGGL((k_pass<true, kPackedRow>), dim3(grid), dim3(kPassThreads), 0, 0, a);
+            });
 #define P(ABL, TXT)                                                                                       \
     snprintf(nm, sizeof nm, "F%d PB%d %s", 1 << fb, 1 << pbl, TXT);                                       \
-    run(nm, [&] { hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a); })
-            P(1, "no bucket atomic");
+    run(nm, [&] {                                                                                          \
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);                    \
+        hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a);     \
+    })
             P(2, "synthetic rows");
             P(4, "no row stores");
             P(6, "synthetic rows, no stores");
@@ -86,7 +94,7 @@ int main() {
             CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
             CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
             a.prof = prof;
-            CK(hipMemset(nb, 0, 4));
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);
             hipLaunchKernelGGL((k_pass<true, kPackedRow, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a);
             CK(hipDeviceSynchronize());
             std::vector<u64> h(grid * 8);
@@ -136,6 +144,7 @@ int main() {
         CK(hipMalloc(&ws.tile_start, (P2 + 1) * 4));
         CK(hipMalloc(&ws.tile_owner, radix_tiles((long long)n, P2) * 4));
         CK(hipMalloc(&ws.tdesc, radix_tiles((long long)n, P2) * 16));
+        CK(hipMalloc(&ws.wstart, 1025 * 4));
         CK(hipMalloc(&ws.scan_sums, (P2 / 8192 + 2) * 8));
         SrcDev src{};
         src.form = kPacked64;
@@ -173,12 +182,13 @@ int main() {
         b.bfill = bfill;
         b.nb = nb;
         b.max_buckets = (unsigned)maxb;
+        b.wstart = wst;
         b.out_pbl = kFinalPbl;
         b.fbits = 8;
         b.shift = 64 - 17;
         {
             // correctness: every row must land in the pass-2 output exactly once
-            CK(hipMemset(nb, 0, 4));
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
             hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b);
             CK(hipDeviceSynchronize());
             unsigned nbh = 0;
@@ -199,21 +209,28 @@ int main() {
             printf("pass-2 check: %u bucket ids, %llu used, %llu rows out of %llu (%s); descriptors cover %llu runs of %llu\n",
                    nbh, used, rows, n, rows == n ? "ok" : "MISMATCH", druns, nruns);
         }
-        run("pass 2 (F256 PB256, runs) k_pass", [&] { hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b); });
-#define P2X(ABL, TXT) run("pass 2 " TXT, [&] { hipLaunchKernelGGL((k_pass<true, kBucketed, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b); })
-        P2X(1, "no bucket atomic");
+        auto p2 = [&] {
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
+            hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b);
+        };
+        run("pass 2 (F256 PB256, runs) k_pass", p2);
+#define P2X(ABL, TXT)                                                                                  \
+    run("pass 2 " TXT, [&] {                                                                             \
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);                    \
+        hipLaunchKernelGGL((k_pass<true, kBucketed, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b);     \
+    })
         P2X(2, "synthetic rows");
         P2X(4, "no row stores");
         P2X(6, "synthetic rows, no stores");
 #undef P2X
         b.out_pbl = kPassPbl;
-        run("pass 2 with 512-row output buckets", [&] { hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b); });
+        run("pass 2 with 512-row output buckets", p2);
         b.out_pbl = kFinalPbl;
         u64 *prof;
         CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
         CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
         b.prof = prof;
-        CK(hipMemset(nb, 0, 4));
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
         hipLaunchKernelGGL((k_pass<true, kBucketed, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b);
         CK(hipDeviceSynchronize());
         std::vector<u64> h(grid * 8);
