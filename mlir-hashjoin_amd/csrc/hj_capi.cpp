@@ -87,7 +87,7 @@ struct Buf {
 
 // Device buffers of one radix bucket set (hj::BucketSet).
 struct SetBufs {
-    Buf rows, bbin, bfill, blist, pstart, runs, rstart;
+    Buf rows, bbin, bfill, runs, rstart;
     unsigned max_buckets = 0;
     unsigned long long max_rows = 0;
     unsigned long long max_runs = 0;
@@ -205,13 +205,10 @@ int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
     HJ_TRY(ensure_buf(sb.rows, (size_t)need.rows * esz));
     HJ_TRY(ensure_buf(sb.bbin, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.bfill, (size_t)need.buckets * 4));
-    HJ_TRY(ensure_buf(sb.blist, (size_t)need.buckets * 8));
-    HJ_TRY(ensure_buf(sb.pstart, (P + 1) * 8));
     HJ_TRY(ensure_buf(sb.rstart, (P + 1) * 8));
     // capacity actually held (buffers may be larger than this need)
     size_t cap = sb.bbin.bytes / 4;
     if (sb.bfill.bytes / 4 < cap) cap = sb.bfill.bytes / 4;
-    if (sb.blist.bytes / 8 < cap) cap = sb.blist.bytes / 8;
     sb.max_buckets = (unsigned)(cap < 0xFFFFFFF0ull ? cap : 0xFFFFFFF0ull);
     sb.max_rows = sb.rows.bytes / esz;
     // a bucket of f rows lists ceil(f / 64) runs: <= rows / 64 + buckets
@@ -225,8 +222,6 @@ hj::BucketSet bucket_set(SetBufs &sb) {
     b.rows = sb.rows.p;
     b.bbin = (unsigned *)sb.bbin.p;
     b.bfill = (unsigned *)sb.bfill.p;
-    b.blist = (unsigned long long *)sb.blist.p;
-    b.pstart = (unsigned long long *)sb.pstart.p;
     b.runs = (unsigned long long *)sb.runs.p;
     b.rstart = (unsigned long long *)sb.rstart.p;
     b.max_buckets = sb.max_buckets;
@@ -395,8 +390,8 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         xs.key = c->sset.rows.p;
         xs.pay = nullptr;
         xs.form = hj::kXcdRows;
-        xs.list = (const unsigned long long *)c->sset.blist.p;
-        xs.pstart = (const unsigned long long *)c->sset.pstart.p;
+        xs.runs = (const unsigned long long *)c->sset.runs.p;
+        xs.rstart = (const unsigned long long *)c->sset.rstart.p;
         HJ_HIP(hj::launch_probe(table_dev(c), layout, xs, out, count_only, (unsigned *)c->slow.p, st));
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
@@ -807,7 +802,7 @@ void hj_ctx_destroy(hj_ctx *c) {
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
-        for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->blist, &sb->pstart, &sb->runs, &sb->rstart}) free_buf(*b);
+        for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->runs, &sb->rstart}) free_buf(*b);
     for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums,
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums})
         free_buf(*b);

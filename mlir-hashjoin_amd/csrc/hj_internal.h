@@ -56,8 +56,8 @@ struct SrcDev {
     long long n;
     long long row_base; // kCol32: row id = row_base + row
     int form;
-    const unsigned long long *list = nullptr;     // kXcdRows: bucket << 32 | fill, grouped
-    const unsigned long long *pstart = nullptr;   // kXcdRows: 9 group starts into list
+    const unsigned long long *runs = nullptr;     // kXcdRows: runs (row << 7 | count), grouped
+    const unsigned long long *rstart = nullptr;   // kXcdRows: 9 group starts into runs
 };
 constexpr int kXcdPbl = 9;        // rows per bucket of a kXcdRows probe side (log2)
 constexpr int kXcdGroups = 8;     // one per XCD
@@ -91,22 +91,18 @@ struct RadixPlan {
 };
 
 // One pass's output: packed rows in buckets of 2^pbl rows; bucket j holds
-// bfill[j] rows of partition bbin[j].  After the pass, blist lists the
-// buckets grouped by partition as (j << 32 | bfill[j]): partition p owns
-// blist[pstart[p] .. pstart[p+1]).  The same rows are also listed as RUNS
-// of <= 64 consecutive rows of one bucket (row << 7 | count; a bucket of f
-// rows gives ceil(f / 64) runs), grouped by partition: p owns
-// runs[rstart[p] .. rstart[p+1]).  Consumers that map one wave to 64 rows
-// read runs, so a partly filled bucket idles at most one wave's tail.
+// bfill[j] rows of partition bbin[j].  After the pass the rows are listed
+// as RUNS of <= 64 consecutive rows of one bucket (row << 7 | count; a
+// bucket of f rows gives ceil(f / 64) runs), grouped by partition: p owns
+// runs[rstart[p] .. rstart[p+1]).  Consumers map one wave to one run, so a
+// partly filled bucket idles at most one wave's tail.
 constexpr int kRunLog = 6;
 struct BucketSet {
     void *rows;                    // >= max_buckets << pbl rows
     unsigned *bbin, *bfill;        // >= max_buckets
-    unsigned long long *blist;     // >= max_buckets
-    unsigned long long *pstart;    // >= P + 1 (P of the pass writing the set)
     unsigned long long *runs;      // >= max_runs
-    unsigned long long *rstart;    // >= P + 1
-    unsigned max_buckets;          // bbin / bfill / blist entries
+    unsigned long long *rstart;    // >= P + 1 (P of the pass writing the set)
+    unsigned max_buckets;          // bbin / bfill entries
     unsigned long long max_rows;   // rows entries
     unsigned long long max_runs;   // runs entries (max_rows / 64 + max_buckets covers any fill)
 };
@@ -114,7 +110,7 @@ struct BucketSet {
 struct RadixWork {                 // scratch shared by the partition passes
     BucketSet tmp;                 // ping set of multi-pass plans
     unsigned *nb;                  // device bucket counter
-    unsigned long long *pcur;      // >= P + 1: list placement cursors / chunk-map scratch
+    unsigned long long *pcur;      // >= P + 1: chunk-map scratch
     unsigned long long *rcur;      // >= P + 1: run placement cursors
     unsigned *tile_start;          // >= P + 1
     unsigned *tile_owner;          // >= radix_tiles(n, P)

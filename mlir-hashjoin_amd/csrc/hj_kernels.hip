@@ -165,21 +165,21 @@ __global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
 
 // ------------------------------------------------------------------ probe tiles
 // A probe tile is kProbeItems * kBlock rows.  Plain sources: tile q = rows
-// [q * kTile, ...).  kXcdRows: tile (g, q) = buckets 4q .. 4q+3 of group g.
+// [q * kTile, ...).  kXcdRows: tile (g, q) = runs 32q .. 32q+31 of group g.
 constexpr int kProbeTile = kBlock * kProbeItems;
-constexpr int kXcdTileBuckets = kProbeTile >> kXcdPbl;
-static_assert(kXcdTileBuckets * (1 << kXcdPbl) == kProbeTile, "tile = whole buckets");
+constexpr int kXcdTileRuns = kProbeTile >> kRunLog;
+static_assert(kXcdTileRuns * (1 << kRunLog) == kProbeTile, "tile = whole runs");
 
 template <int L, int FORM>
 __device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned g, unsigned long long q, int i, Tuple &tp) {
     if constexpr (FORM == kXcdRows) {
         const unsigned v = (unsigned)i * kBlock + threadIdx.x;
-        const unsigned long long li = src.pstart[g] + q * kXcdTileBuckets + (v >> kXcdPbl);
-        if (li >= src.pstart[g + 1]) return false;
-        const unsigned long long e = src.list[li];
-        const unsigned off = v & ((1u << kXcdPbl) - 1u);
-        if (off >= (unsigned)e) return false;
-        const unsigned long long r = ((e >> 32) << kXcdPbl) + off;
+        const unsigned long long li = src.rstart[g] + q * kXcdTileRuns + (v >> kRunLog);
+        if (li >= src.rstart[g + 1]) return false;
+        const unsigned long long e = src.runs[li];
+        const unsigned off = v & ((1u << kRunLog) - 1u);
+        if (off >= (unsigned)(e & 127u)) return false;
+        const unsigned long long r = (e >> 7) + off;
         if constexpr (L == kWide) {
             const ulonglong2 x = ((const ulonglong2 *)src.key)[r];
             tp = Tuple{x.x, x.y};
@@ -204,7 +204,7 @@ __device__ __forceinline__ void probe_tiles(const SrcDev &src, unsigned &g, unsi
         g = blockIdx.x % kXcdGroups;   // round-robin block -> XCD deal: group g stays in one XCD's L2
         q0 = blockIdx.x / kXcdGroups;
         step = gridDim.x / kXcdGroups;
-        nt = (src.pstart[g + 1] - src.pstart[g] + kXcdTileBuckets - 1) / kXcdTileBuckets;
+        nt = (src.rstart[g + 1] - src.rstart[g] + kXcdTileRuns - 1) / kXcdTileRuns;
     } else {
         g = 0;
         q0 = blockIdx.x;

@@ -630,56 +630,47 @@ __global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, uns
     if (w == G) *a.nb = (unsigned)(tot < a.max_buckets ? tot : a.max_buckets);
 }
 
-// Bucket list by partition: count buckets (and their runs) per partition,
-// exclusive scans (k_scan_*), then place every bucket id and its runs at its
-// partition's cursors.  Blocks aggregate in LDS first when partitions are
+// Runs by partition: count the runs of every bucket per partition,
+// exclusive scan (k_scan_*), then place each bucket's runs at its
+// partition's cursor.  Blocks aggregate in LDS first when partitions are
 // few (pass 1: 512).
 constexpr int kListPer = 4;
 constexpr int kListLds = 4096;
 
 __device__ __forceinline__ unsigned runs_of(unsigned fill) { return (fill + (1u << kRunLog) - 1) >> kRunLog; }
 
-// Buckets [0, *nb) of a pass, clamped to the set's capacity (the counter
-// passes it only when a pass ran out of buckets, which radix_need excludes).
+// Buckets [0, *nb) of a pass, clamped to the set's capacity; holes (unused
+// ids of a workgroup's range) are kNoBucket.
 __global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, u64 *pcnt, u64 *rcnt, int P) {
-    __shared__ unsigned c[kListLds], cr[kListLds];
+                                                 unsigned max_buckets, u64 *rcnt, int P) {
+    __shared__ unsigned cr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
     const bool lds = P <= kListLds;
     if (lds)
-        for (int i = threadIdx.x; i < P; i += 1024) c[i] = cr[i] = 0u;
+        for (int i = threadIdx.x; i < P; i += 1024) cr[i] = 0u;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         const unsigned b = j < n ? bbin[j] : kNoBucket;
-        if (b < (unsigned)P) {   // holes (unused pool ids) are kNoBucket
+        if (b < (unsigned)P) {
             const unsigned nr = runs_of(bfill[j]);
-            if (lds) {
-                atomicAdd(&c[b], 1u);
-                atomicAdd(&cr[b], nr);
-            } else {
-                atomicAdd(&pcnt[b], 1ull);
-                atomicAdd(&rcnt[b], (u64)nr);
-            }
+            if (lds) atomicAdd(&cr[b], nr);
+            else atomicAdd(&rcnt[b], (u64)nr);
         }
     }
     if (!lds) return;
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += 1024)
-        if (c[i]) {
-            atomicAdd(&pcnt[i], (u64)c[i]);
-            atomicAdd(&rcnt[i], (u64)cr[i]);
-        }
+        if (cr[i]) atomicAdd(&rcnt[i], (u64)cr[i]);
 }
 
 __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, int pbl, u64 *pcur, u64 *rcur, u64 *blist,
-                                                 u64 *runs, int P) {
-    __shared__ unsigned c[kListLds], cr[kListLds];
-    __shared__ u64 cb[kListLds], cbr[kListLds];
+                                                 unsigned max_buckets, int pbl, u64 *rcur, u64 *runs, int P) {
+    __shared__ unsigned cr[kListLds];
+    __shared__ u64 cbr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
@@ -697,39 +688,30 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
             const unsigned b = j < n ? bbin[j] : kNoBucket;
             if (b < (unsigned)P) {
                 const unsigned f = bfill[j];
-                blist[atomicAdd(&pcur[b], 1ull)] = (j << 32) | f;
                 put_runs(j, f, atomicAdd(&rcur[b], (u64)runs_of(f)));
             }
         }
         return;
     }
-    for (int i = threadIdx.x; i < P; i += 1024) c[i] = cr[i] = 0u;
+    for (int i = threadIdx.x; i < P; i += 1024) cr[i] = 0u;
     __syncthreads();
-    unsigned rk[kListPer], rr[kListPer], bn[kListPer], fl[kListPer];
+    unsigned rr[kListPer], bn[kListPer], fl[kListPer];
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         bn[i] = j < n ? bbin[j] : kNoBucket;
         if (bn[i] >= (unsigned)P) bn[i] = kNoBucket;
         fl[i] = bn[i] != kNoBucket ? bfill[j] : 0u;
-        if (bn[i] != kNoBucket) {
-            rk[i] = atomicAdd(&c[bn[i]], 1u);
-            rr[i] = atomicAdd(&cr[bn[i]], runs_of(fl[i]));
-        }
+        if (bn[i] != kNoBucket) rr[i] = atomicAdd(&cr[bn[i]], runs_of(fl[i]));
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += 1024)
-        if (c[i]) {
-            cb[i] = atomicAdd(&pcur[i], (u64)c[i]);
-            cbr[i] = atomicAdd(&rcur[i], (u64)cr[i]);
-        }
+        if (cr[i]) cbr[i] = atomicAdd(&rcur[i], (u64)cr[i]);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
-        if (bn[i] == kNoBucket) continue;
-        blist[cb[bn[i]] + rk[i]] = (j << 32) | fl[i];
-        put_runs(j, fl[i], cbr[bn[i]] + rr[i]);
+        if (bn[i] != kNoBucket) put_runs(j, fl[i], cbr[bn[i]] + rr[i]);
     }
 }
 
@@ -1271,7 +1253,7 @@ unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_ru
 }
 
 // Partition one relation into the plan's 2^total_bits partitions: bucket
-// rows in `out` (with blist / pstart by partition).  ws.tmp is the ping set
+// rows in `out` (with runs / rstart by partition).  ws.tmp is the ping set
 // of multi-pass plans.  Asynchronous; no allocation.
 hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
                            const BucketSet &out, hipStream_t st) {
@@ -1338,28 +1320,21 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
             }
 #undef HJ_PASS
         }
-        // list the buckets and their runs by partition: pstart / rstart =
-        // scans of per-partition counts
+        // list the runs by partition: rstart = scan of per-partition counts
         const u64 P = (u64)nseg << fb;
-        e = hipMemsetAsync(dst.pstart, 0, (P + 1) * sizeof(u64), st);
-        if (e != hipSuccess) return e;
         e = hipMemsetAsync(dst.rstart, 0, (P + 1) * sizeof(u64), st);
         if (e != hipSuccess) return e;
         // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
         if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
         const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
         hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, dst.pstart, dst.rstart,
-                           (int)P);
-        scan_u64(dst.pstart, P + 1, ws.scan_sums, st);
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, dst.rstart, (int)P);
         scan_u64(dst.rstart, P + 1, ws.scan_sums, st);
-        e = hipMemcpyAsync(ws.pcur, dst.pstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
         e = hipMemcpyAsync(ws.rcur, dst.rstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass], ws.pcur,
-                           ws.rcur, dst.blist, dst.runs, (int)P);
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass], ws.rcur,
+                           dst.runs, (int)P);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         prev = &dst;

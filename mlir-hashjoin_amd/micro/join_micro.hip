@@ -39,8 +39,6 @@ BucketSet make_set(RadixNeed nd, int P) {
     b.rows = dalloc<ulonglong2>(nd.rows);
     b.bbin = dalloc<unsigned>(nd.buckets);
     b.bfill = dalloc<unsigned>(nd.buckets);
-    b.blist = dalloc<u64>(nd.buckets);
-    b.pstart = dalloc<u64>((u64)P + 1);
     b.rstart = dalloc<u64>((u64)P + 1);
     b.max_buckets = (unsigned)nd.buckets;
     b.max_rows = nd.rows;
@@ -78,30 +76,28 @@ int main() {
     src.key = s;
     CK(radix_partition(src, true, pl, ws, ss, 0));
     CK(hipDeviceSynchronize());
-    // fill statistics
+    // run statistics of the final sets
     for (int side = 0; side < 2; ++side) {
         const BucketSet &b = side ? ss : rs;
         std::vector<u64> ps(P + 1);
-        CK(hipMemcpy(ps.data(), b.pstart, (P + 1) * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(ps.data(), b.rstart, (P + 1) * 8, hipMemcpyDeviceToHost));
         std::vector<u64> lst(ps[P]);
-        CK(hipMemcpy(lst.data(), b.blist, ps[P] * 8, hipMemcpyDeviceToHost));
-        u64 rows = 0, part = 0, maxb = 0, over8 = 0, over10 = 0, maxrows = 0;
+        CK(hipMemcpy(lst.data(), b.runs, ps[P] * 8, hipMemcpyDeviceToHost));
+        u64 rows = 0, part = 0, maxr = 0, maxrows = 0;
         for (int p = 0; p < P; ++p) {
             u64 pr = 0;
             for (u64 i = ps[p]; i < ps[p + 1]; ++i) {
-                const unsigned f = (unsigned)lst[i];
+                const unsigned f = (unsigned)(lst[i] & 127u);
                 pr += f;
-                part += f < 256;
+                part += f < 64;
             }
             rows += pr;
-            const u64 nbk = ps[p + 1] - ps[p];
-            maxb = nbk > maxb ? nbk : maxb;
+            const u64 nr = ps[p + 1] - ps[p];
+            maxr = nr > maxr ? nr : maxr;
             maxrows = pr > maxrows ? pr : maxrows;
-            over8 += nbk > 8;
-            over10 += nbk > 10;
         }
-        printf("%s: buckets %llu rows %llu partial %llu (%.2f/partition) max buckets %llu max rows %llu  >8 bk %.1f%%  >10 bk %.1f%%\n",
-               side ? "S" : "R", ps[P], rows, part, (double)part / P, maxb, maxrows, 100.0 * over8 / P, 100.0 * over10 / P);
+        printf("%s: runs %llu rows %llu partial runs %llu (%.2f/partition) max runs %llu max rows %llu\n",
+               side ? "S" : "R", ps[P], rows, part, (double)part / P, maxr, maxrows);
     }
     unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_runs));
     void *desc = dalloc<char>(radix_join_items(pl, ss.max_runs) * radix_item_desc_bytes());

@@ -129,8 +129,6 @@ int main() {
         CK(hipMalloc(&b1.rows, nd.rows * 16));
         CK(hipMalloc(&b1.bbin, nd.buckets * 4));
         CK(hipMalloc(&b1.bfill, nd.buckets * 4));
-        CK(hipMalloc(&b1.blist, nd.buckets * 8));
-        CK(hipMalloc(&b1.pstart, (P1 + 1) * 8));
         CK(hipMalloc(&b1.rstart, (P1 + 1) * 8));
         b1.max_buckets = (unsigned)nd.buckets;
         b1.max_rows = nd.rows;
@@ -161,11 +159,10 @@ int main() {
         }
         CK(hipDeviceSynchronize());
         unsigned ntiles = 0;
-        u64 nruns = 0, nbk = 0;
+        u64 nruns = 0;
         CK(hipMemcpy(&ntiles, ws.tile_start + P1, 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(&nruns, b1.rstart + P1, 8, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(&nbk, b1.pstart + P1, 8, hipMemcpyDeviceToHost));
-        printf("pass-1 set: %llu buckets, %llu runs (%.3f x n/64), %u pass-2 tiles (%.3f x n/4096)\n", nbk, nruns,
+        printf("pass-1 set: %llu runs (%.3f x n/64), %u pass-2 tiles (%.3f x n/4096)\n", nruns,
                nruns / (double)(n >> 6), ntiles, ntiles / (double)(n >> 12));
         PassArgs b{};
         b.n = n;
