@@ -89,7 +89,10 @@ int hj_ctx_set_radix_bits(hj_ctx *ctx, int bits);
  * mode: -1 automatic (default; env HJ_XCD=0/1 overrides -- automatic is
  * currently "never"), 0 never, 1 always. */
 int hj_ctx_set_xcd_split(hj_ctx *ctx, int mode);
-/* Strategy the current build uses (HJ_STRATEGY_GLOBAL / _RADIX), 0 if none. */
+/* Strategy of the last probe since the current build (else of the build):
+ * HJ_STRATEGY_GLOBAL / _RADIX, 0 if none.  Under HJ_STRATEGY_AUTO a build side
+ * of [2^18, 2^21) rows gets the global table AND a radix partition; a probe
+ * side of >= 2^24 rows then takes the radix join. */
 int hj_ctx_strategy_used(const hj_ctx *ctx);
 /* GLOBAL: slot capacity of the table (power of two, >= 2 x build rows);
  * RADIX: number of partitions. */

@@ -79,6 +79,13 @@ enum Ev { kEvInit0, kEvInit1, kEvBuild1, kEvProbe0, kEvProbeMid, kEvProbe1, kEvP
 // Build sides at least this large use the radix-partitioned join (LDS
 // tables); smaller ones a global linear-probing table (HJ_STRATEGY_AUTO).
 constexpr int64_t kRadixMinRows = 1ll << 21;
+// AUTO with a smaller build side whose global table outgrows one XCD's L2
+// (>= 2^18 rows = 8 MiB of slots) also radix-partitions R at build time
+// (~20 us); a probe side of >= 2^24 rows then takes the radix join: the
+// global probe of a MALL-resident table is latency-bound (~40 G rows/s,
+// C2 26.4 ms) while partition + LDS join streams (C2 19.7 ms).
+constexpr int64_t kDualMinBuildRows = 1ll << 18;
+constexpr int64_t kRadixProbeMinRows = 1ll << 24;
 
 struct Buf {
     void *p = nullptr;
@@ -111,6 +118,8 @@ struct hj_ctx {
     int radix_bits = 0;                // 0: planner chooses
     int xcd_mode = -1;                 // global-table probe XCD split: -1 auto, 0 off, 1 on
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
+    bool dual = false;                 // global build whose R is ALSO radix-partitioned (probe-time choice)
+    int probe_used = -1;               // strategy of the last probe (-1: none since the build)
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
@@ -280,7 +289,9 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->layout = layout;
     c->n_build = src.n;
     c->used = choose_strategy(c, src.n);
-    if (c->used == HJ_STRATEGY_RADIX) {
+    c->probe_used = -1;
+    c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
+    if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
         // per partition in LDS at probe time)
         const bool wide = layout == kWide;
@@ -293,16 +304,18 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         trace("build: workspace", st, src.n);
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->rset), st));
         trace("build: R partitioned", st, (long long)c->plan.total_bits);
-        record(c, kEvBuild1, st);
-        c->rec[0] = c->rec[1] = c->timing;
-        return HJ_OK;
+        if (!c->dual) {
+            record(c, kEvBuild1, st);
+            c->rec[0] = c->rec[1] = c->timing;
+            return HJ_OK;
+        }
     }
     HJ_TRY(ensure_table(c, src.n, layout));
     c->bits = table_bits(src.n);
     const hj::TableDev t = table_dev(c);
-    record(c, kEvInit0, st);
+    if (!c->dual) record(c, kEvInit0, st);   // (dual: the build phase starts at R's partition)
     HJ_HIP(hj::launch_init(t, layout, 1ull << c->bits, st));
-    record(c, kEvInit1, st);
+    if (!c->dual) record(c, kEvInit1, st);
     HJ_HIP(hj::launch_build(t, layout, src, st));
     record(c, kEvBuild1, st);
     c->rec[0] = c->rec[1] = c->timing;
@@ -350,7 +363,9 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     if (!count_only && (cap < 0 || (cap > 0 && (!out_r || !out_s)))) HJ_FAIL(HJ_ERR_ARG, "bad output");
     HJ_TRY(set_device(c));
     HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
-    if (c->used == HJ_STRATEGY_RADIX) {
+    const bool radix = c->used == HJ_STRATEGY_RADIX || (c->dual && src.n >= kRadixProbeMinRows);
+    c->probe_used = radix ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
+    if (radix) {
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;
         trace("probe: enter", st, src.n);
@@ -824,9 +839,11 @@ int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
     if (max_build_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
     HJ_TRY(set_device(c));
     HJ_TRY(ensure_meta(c, 64));
-    if (choose_strategy(c, max_build_rows) == HJ_STRATEGY_GLOBAL)
-        return ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow);
     const size_t esz = key_bits == 64 ? 16 : 8;
+    if (choose_strategy(c, max_build_rows) == HJ_STRATEGY_GLOBAL) {
+        HJ_TRY(ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow));
+        if (c->strategy != HJ_STRATEGY_AUTO || max_build_rows < kDualMinBuildRows) return HJ_OK;
+    }
     const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits);
     return ensure_radix_scratch(c, c->rset, max_build_rows, esz, pl);
 }
@@ -839,7 +856,7 @@ int64_t hj_ctx_table_capacity(const hj_ctx *c) {
 
 int hj_ctx_radix_plan(const hj_ctx *c, int *passes, int bits[3]) {
     if (!c || !passes || !bits) HJ_FAIL(HJ_ERR_ARG, "null argument");
-    const bool radix = c->layout >= 0 && c->used == HJ_STRATEGY_RADIX;
+    const bool radix = c->layout >= 0 && (c->used == HJ_STRATEGY_RADIX || c->dual);
     *passes = radix ? c->plan.passes : 0;
     for (int i = 0; i < 3; ++i) bits[i] = radix ? c->plan.bits[i] : 0;
     return HJ_OK;
@@ -920,12 +937,15 @@ int hj_ctx_set_xcd_split(hj_ctx *c, int mode) {
     return HJ_OK;
 }
 
-int hj_ctx_strategy_used(const hj_ctx *c) { return (c && c->layout >= 0) ? c->used : 0; }
+int hj_ctx_strategy_used(const hj_ctx *c) {
+    if (!c || c->layout < 0) return 0;
+    return c->probe_used >= 0 ? c->probe_used : c->used;
+}
 
 int hj_ctx_reserve_probe(hj_ctx *c, int64_t max_probe_rows, int key_bits) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     if (max_probe_rows < 0 || (key_bits != 32 && key_bits != 64)) HJ_FAIL(HJ_ERR_ARG, "bad reserve arguments");
-    if (c->layout < 0 || c->used != HJ_STRATEGY_RADIX) return HJ_OK;   // the global table needs no probe workspace
+    if (c->layout < 0 || (c->used != HJ_STRATEGY_RADIX && !c->dual)) return HJ_OK;   // the global table needs none
     HJ_TRY(set_device(c));
     const size_t esz = key_bits == 64 ? 16 : 8;
     return ensure_radix_scratch(c, c->sset, max_probe_rows, esz, c->plan);
