@@ -78,6 +78,42 @@ struct Row<false> {   // i32 key (zero-extended) / i32 row id, packed key << 32 
     static __device__ __forceinline__ T zero() { return 0ull; }
 };
 
+// Streaming (non-temporal) loads/stores for data touched once per kernel:
+// HJ_NT bit 1 pass loads, 2 pass stores, 4 join loads, 8 join stores.
+#ifndef HJ_NT
+#define HJ_NT 12   // measured: join loads + stores nt -2.7 % (profiles/r01_nt_variants.txt); pass stores nt +66 %, pass loads nt +3 %
+#endif
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_s(const T *p) {
+    if constexpr (!NT) {
+        return *p;
+    } else if constexpr (sizeof(T) == 16) {
+        const v2u64 x = __builtin_nontemporal_load((const v2u64 *)p);
+        T r;
+        r.x = x.x;
+        r.y = x.y;
+        return r;
+    } else {
+        return __builtin_nontemporal_load(p);
+    }
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_s(T *p, const T &v) {
+    if constexpr (!NT) {
+        *p = v;
+    } else if constexpr (sizeof(T) == 16) {
+        v2u64 x;
+        x.x = v.x;
+        x.y = v.y;
+        __builtin_nontemporal_store(x, (v2u64 *)p);
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+}
+constexpr bool kNtPassLd = (HJ_NT & 1) != 0, kNtPassSt = (HJ_NT & 2) != 0;
+constexpr bool kNtJoinLd = (HJ_NT & 4) != 0, kNtJoinSt = (HJ_NT & 8) != 0;
+
 // Row `row` of a pass input in form FORM.
 template <bool WIDE, int FORM>
 __device__ __forceinline__ typename Row<WIDE>::T load_row(const SrcDev &s, long long row) {
@@ -344,8 +380,8 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 const u64 r = tlo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
                 const bool v0 = r < a.n, v1 = r + 1 < a.n;
                 if (a.cols_aligned && v1) {
-                    const ulonglong2 k2 = *(const ulonglong2 *)(kc + r);
-                    const ulonglong2 p2 = *(const ulonglong2 *)(pc + r);
+                    const ulonglong2 k2 = ld_s<kNtPassLd>((const ulonglong2 *)(kc + r));
+                    const ulonglong2 p2 = ld_s<kNtPassLd>((const ulonglong2 *)(pc + r));
                     row[2 * i] = R::make(k2.x, p2.x);
                     row[2 * i + 1] = R::make(k2.y, p2.y);
                 } else {
@@ -395,7 +431,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const u64 e = ((u64)(unsigned)__builtin_amdgcn_readlane(ehi, src) << 32) |
                           (u64)(unsigned)__builtin_amdgcn_readlane(elo, src);
             if (lane < (unsigned)(e & 127u) && (e >> 7) + lane < a.in_max_rows) {
-                row[i] = ((const T *)a.in_rows)[(e >> 7) + lane];
+                row[i] = ld_s<kNtPassLd>((const T *)a.in_rows + (e >> 7) + lane);
                 br[i] = 0u;
             } else {
                 row[i] = R::zero();
@@ -546,7 +582,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                 continue;
             }
             const u64 o = slot(b, p);
-            if ((ABL & 4) == 0 && o != ~0ull) out[o] = stage[j];
+            if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, stage[j]);
         }
         for (unsigned q = threadIdx.x; q < F * (L - 1); q += kPassThreads) {
             const unsigned b = q / (L - 1), i = q - b * (L - 1);
@@ -555,7 +591,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const unsigned p = f - tl0 + i;
             if (p >= ((f + cnt[b]) & ~(L - 1))) continue;   // line still incomplete: stays
             const u64 o = slot(b, p);
-            if ((ABL & 4) == 0 && o != ~0ull) out[o] = tail[q];
+            if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, tail[q]);
         }
         __syncthreads();
         mark(3);
@@ -814,7 +850,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
 #pragma unroll
         for (int i = 0; i < n; ++i) {
             if (off < (unsigned)(e[i] & 127u)) {
-                v[i] = rows[(e[i] >> 7) + off];
+                v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + off);
                 ok |= 1u << i;
             } else {
                 v[i] = R::zero();
@@ -1025,8 +1061,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                         if (m[i] == 0xFFFFFFFFu) continue;
                         const u64 pos = s_base + s_cw[i * NW + wv] + lpre[i];
                         if (pos < (u64)a.cap) {
-                            orr[pos] = WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull);
-                            oss[pos] = (PT)R::pay(sv_[i]);
+                            st_s<kNtJoinSt>(orr + pos, WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull));
+                            st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
                         }
                     }
                     __syncthreads();   // s_cw / s_base reused by the next sub-chunk
