@@ -180,3 +180,32 @@ def test_radix_c3_2p28(hj):
     assert o_r.numel() == n
     assert bool((rk[o_r] == sk[o_s]).all())
     assert torch.equal(torch.sort(o_s)[0], torch.arange(n, device="cuda"))
+
+
+def test_radix_many_subchunk_items(hj, oracle):
+    """Small R, long S: each work item probes one LDS table with many
+    2560-row sub-chunks, and a partition's S spans several items."""
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(31, 3000, 400000, 0.9)
+    o = run(hj, rk, rp, sk, sp, 1)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=300))
+
+
+def test_auto_probe_time_strategy(hj):
+    """AUTO with a build side in [2^18, 2^21): the global table is built AND
+    R is radix-partitioned; a probe side >= 2^24 rows takes the radix join,
+    a smaller one the global table -- same pairs either way."""
+    nr = 1 << 18
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EED, nr, 1 << 24, 0.95)
+    hj.set_strategy("auto")
+    res = {}
+    for ns in (1 << 20, 1 << 24):
+        o_r, o_s = hj.join(rk, rp, sk[:ns], sp[:ns])
+        res[ns] = hj.strategy_used
+        order = torch.argsort(o_s)
+        hj.set_strategy("global")
+        g_r, g_s = hj.join(rk, rp, sk[:ns], sp[:ns])
+        hj.set_strategy("auto")
+        gorder = torch.argsort(g_s)
+        assert o_r.numel() == g_r.numel()
+        assert torch.equal(o_r[order], g_r[gorder]) and torch.equal(o_s[order], g_s[gorder])
+    assert res == {1 << 20: "global", 1 << 24: "radix"}
