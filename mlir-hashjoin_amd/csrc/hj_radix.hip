@@ -51,8 +51,8 @@ constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build 
 constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
 constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
-constexpr int kPassPbl = 9;        // 512-row buckets for intermediate passes
-constexpr int kFinalPbl = 8;       // 256-row buckets for the join's input (less slack)
+constexpr int kPassPbl = 10;       // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
+constexpr int kFinalPbl = 9;       // 512-row buckets for the join's input (8 / 9 / 10+9 measured: profiles/r01_bucket_sizes.txt)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
 
