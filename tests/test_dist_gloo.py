@@ -78,7 +78,8 @@ def _worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=7, NS=3, frac=1.0, seed=13),             # tiny / ragged
     dict(dist="pkfk", NR=3001, NS=4999, frac=0.7, seed=14, max_rows=97),  # slices cut in pieces
     dict(dist="pkfk", NR=4000, NS=6001, frac=0.9, seed=15, max_rows=300, world=3),
-], ids=["pkfk", "uniform_dups", "tiny", "pieces", "three_ranks_pieces"])
+    dict(dist="uniform", NR=5000, NS=7001, hi=900, seed=16, max_rows=211, world=4),
+], ids=["pkfk", "uniform_dups", "tiny", "pieces", "three_ranks_pieces", "four_ranks_dups_pieces"])
 def test_two_rank_exchange_join(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
