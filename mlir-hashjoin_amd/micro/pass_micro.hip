@@ -7,6 +7,7 @@
 #include "../csrc/hj_radix.hip"
 
 #include <cstdio>
+#include <algorithm>
 #include <vector>
 #ifndef PHASE_ABL
 #define PHASE_ABL 8
@@ -16,12 +17,21 @@
 using namespace hj;
 typedef unsigned long long u64;
 
-__global__ void k_fill(ulonglong2 *r, u64 n) {
+// skew: about 3 % of the rows carry one of three hot keys (1.6 / 0.9 /
+// 0.6 %), the top of C4's Zipf(0.9) foreign keys
+__global__ void k_fill(ulonglong2 *r, u64 n, int skew) {
     const u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) r[i] = make_ulonglong2(fmix64(i * 7 + 1), i);
+    if (i >= n) return;
+    u64 k = fmix64(i * 7 + 1);
+    if (skew) {
+        const unsigned j = (unsigned)(fmix64(i ^ 0x5EED) % 1000u);
+        if (j < 31) k = j < 16 ? 11ull : (j < 25 ? 22ull : 33ull);
+    }
+    r[i] = make_ulonglong2(k, i);
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const int skew = argc > 1;   // any argument: skewed keys
     const u64 n = 1ull << 28;
     ulonglong2 *in, *out;
     unsigned *bbin, *bfill, *nb;
@@ -31,7 +41,7 @@ int main() {
     CK(hipMalloc(&bbin, maxb * 4));
     CK(hipMalloc(&bfill, maxb * 4));
     CK(hipMalloc(&nb, 64));
-    hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, 0, in, n);
+    hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, 0, in, n, skew);
     CK(hipDeviceSynchronize());
     PassArgs a{};
     a.in.key = in;
@@ -242,6 +252,22 @@ int main() {
             tot += m[k];
         }
         for (int k = 0; k < 5; ++k) printf("  pass 2 phase %-38s %10.0f cycles  %5.1f %%\n", names[k], m[k], 100.0 * m[k] / tot);
+        // the slowest workgroups and their phases (stragglers under skew)
+        std::vector<std::pair<double, unsigned>> wt(grid);
+        for (unsigned g = 0; g < grid; ++g) {
+            double t = 0;
+            for (int k = 0; k < 5; ++k) t += (double)h[g * 8 + k];
+            wt[g] = {t, g};
+        }
+        std::sort(wt.begin(), wt.end());
+        printf("  workgroup totals: min %.0f median %.0f max %.0f cycles\n", wt[0].first, wt[grid / 2].first,
+               wt[grid - 1].first);
+        for (unsigned r = grid - 4; r < grid; ++r) {
+            const unsigned g = wt[r].second;
+            printf("  wg %4u:", g);
+            for (int k = 0; k < 5; ++k) printf(" %10llu", h[g * 8 + k]);
+            printf("\n");
+        }
     }
     return 0;
 }

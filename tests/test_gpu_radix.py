@@ -209,3 +209,18 @@ def test_auto_probe_time_strategy(hj):
         assert o_r.numel() == g_r.numel()
         assert torch.equal(o_r[order], g_r[gorder]) and torch.equal(o_s[order], g_s[gorder])
     assert res == {1 << 20: "global", 1 << 24: "radix"}
+
+
+@pytest.mark.parametrize("bits", [9, 17])
+def test_radix_hot_key_tiles(hj, oracle, bits):
+    """Skewed probe keys: 40 % / 10 % of 2^20 S rows carry two hot keys, so
+    most tiles of a workgroup (>= 8 each) hold a bin of > kTile / 8 rows and
+    k_pass counts that bin's lanes with one atomic per wave instruction."""
+    rng = np.random.default_rng(17)
+    rk = np.arange(65536, dtype=np.int64) * 7; rp = np.arange(65536, dtype=np.int64) + 3
+    n = 1 << 20
+    u = rng.random(n)
+    sk = np.where(u < 0.4, 21, np.where(u < 0.5, 70, rng.integers(0, 65536 * 7, n))).astype(np.int64)
+    sp = np.arange(n, dtype=np.int64)
+    o = run(hj, rk, rp, sk, sp, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=4096))
