@@ -996,6 +996,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                 u64 e0[SI];
                 bool pa[SI];
                 u64 cnt = 0;
+                unsigned mb = 0u;   // general path: bit i = row slot i has a match
 #pragma unroll
                 for (int i = 0; i < SI; ++i) {
                     m[i] = 0xFFFFFFFFu;
@@ -1051,17 +1052,37 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                         }
                     }
                 } else {
+                    // every chain walks to EMPTY (a key may repeat); row
+                    // slots in pairs as above
+                    auto hit = [&](u64 e, u64 key) { return (WIDE ? e : (e >> 32)) == key; };
 #pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if (!pa[i]) continue;
-                        const u64 key = R::key(sv_[i]);
-                        unsigned h = hp[i];
-                        u64 e = e0[i];
-                        while (e != kEmpty) {
-                            if ((WIDE ? e : (e >> 32)) == key) ++cnt;
+                    for (int i = 0; i < SI; i += 2) {
+                        const int j = i + 1 < SI ? i + 1 : i;
+                        const u64 ka = R::key(sv_[i]), kb = R::key(sv_[j]);
+                        unsigned ha = hp[i], hb = hp[j];
+                        u64 ea = e0[i], eb = e0[j];
+                        bool la = pa[i] && ea != kEmpty;
+                        bool lb = j != i && pa[j] && eb != kEmpty;
+                        while (la || lb) {
+                            if (la) {
+                                if (hit(ea, ka)) {
+                                    ++cnt;
+                                    mb |= 1u << i;
+                                }
+                                ha = (ha + 1) & kMask;
+                                ea = tkey[ha];
+                            }
+                            if (lb) {
+                                if (hit(eb, kb)) {
+                                    ++cnt;
+                                    mb |= 1u << j;
+                                }
+                                hb = (hb + 1) & kMask;
+                                eb = tkey[hb];
+                            }
                             if constexpr ((ABL & 16) != 0) break;
-                            h = (h + 1) & kMask;
-                            e = tkey[h];
+                            la = la && ea != kEmpty;
+                            lb = lb && eb != kEmpty;
                         }
                     }
                 }
@@ -1140,7 +1161,9 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                             }
                         } else {
                             const u64 key = R::key(sv_[i]);
-                            if (!((sok >> i) & 1u) || (WIDE && key == kEmptyKey64)) continue;
+                            // rows without a match skip the second walk (with
+                            // duplicate keys most probes still miss: C1-ref)
+                            if (!((mb >> i) & 1u)) continue;
                             unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
                             while (true) {
                                 const u64 e = tkey[h];
