@@ -212,6 +212,18 @@ def test_auto_probe_time_strategy(hj):
 
 
 @pytest.mark.parametrize("bits", [9, 17])
+def test_radix_hot_key_tiles_i32(hj, oracle, bits):
+    """The same skew on the reference types (i32 keys, row-id payloads)."""
+    rng = np.random.default_rng(18)
+    r = (np.arange(65536, dtype=np.int64) * 7 - 200000).astype(np.int32)
+    n = 1 << 20
+    u = rng.random(n)
+    s = np.where(u < 0.45, r[3], np.where(u < 0.55, r[40000], r[rng.integers(0, 65536, n)])).astype(np.int32)
+    o = run(hj, r, None, s, None, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i32(r, s, H=4096))
+
+
+@pytest.mark.parametrize("bits", [9, 17])
 def test_radix_hot_key_tiles(hj, oracle, bits):
     """Skewed probe keys: 40 % / 10 % of 2^20 S rows carry two hot keys, so
     most tiles of a workgroup (>= 8 each) hold a bin of > kTile / 8 rows and
