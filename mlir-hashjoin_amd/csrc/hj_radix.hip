@@ -251,6 +251,10 @@ struct PassArgs {
     int shift;                   // bin = (hash >> shift) & (F - 1)
     int fbits;
     u64 *prof = nullptr;         // diagnostics (ABL & 8): per workgroup, cycles per phase
+    // zeroed by the pass for the listing that follows it (its per-partition
+    // run counts and cursors): two memsets and a copy fewer per pass
+    u64 *zero_a = nullptr, *zero_b = nullptr;
+    u64 zero_n = 0;
 };
 
 // A bucketed pass's tile: runs [lo, lo + cnt) (cnt <= kTile / 64) of segment seg.
@@ -311,6 +315,10 @@ template <bool WIDE, int FORM, int ABL = 0>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
+    for (u64 i = (u64)blockIdx.x * kPassThreads + threadIdx.x; i < a.zero_n; i += (u64)gridDim.x * kPassThreads) {
+        a.zero_a[i] = 0ull;
+        a.zero_b[i] = 0ull;
+    }
     constexpr int IT = kPassRows;
     constexpr unsigned L = 128 / sizeof(T);   // rows per line
     __shared__ T stage[kTile];
@@ -754,7 +762,8 @@ __global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const uns
 }
 
 __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, int pbl, u64 *rcur, u64 *runs, int P) {
+                                                 unsigned max_buckets, int pbl, const u64 *rstart, u64 *rcur,
+                                                 u64 *runs, int P) {
     __shared__ unsigned cr[kListLds];
     __shared__ u64 cbr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
@@ -774,7 +783,7 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
             const unsigned b = j < n ? bbin[j] : kNoBucket;
             if (b < (unsigned)P) {
                 const unsigned f = bfill[j];
-                put_runs(j, f, atomicAdd(&rcur[b], (u64)runs_of(f)));
+                put_runs(j, f, rstart[b] + atomicAdd(&rcur[b], (u64)runs_of(f)));
             }
         }
         return;
@@ -792,7 +801,7 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
     }
     __syncthreads();
     for (int i = threadIdx.x; i < P; i += 1024)
-        if (cr[i]) cbr[i] = atomicAdd(&rcur[i], (u64)cr[i]);
+        if (cr[i]) cbr[i] = rstart[i] + atomicAdd(&rcur[i], (u64)cr[i]);
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
@@ -1413,6 +1422,12 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
             a.tdesc = (const TileDesc *)ws.tdesc;
         }
         a.wstart = ws.wstart;
+        // list the runs by partition afterwards: rstart = scan of the
+        // per-partition run counts, k_bplace's cursors rstart + rcur
+        const u64 P = (u64)nseg << fb;
+        a.zero_a = dst.rstart;
+        a.zero_b = ws.rcur;
+        a.zero_n = n > 0 ? P + 1 : 0;
         if (grid > 1024) return hipErrorInvalidValue;   // k_id_plan: one block
         hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, st, a, prev != nullptr, grid, ws.wstart);
         if (n > 0) {
@@ -1429,21 +1444,20 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
             }
 #undef HJ_PASS
         }
-        // list the runs by partition: rstart = scan of per-partition counts
-        const u64 P = (u64)nseg << fb;
-        e = hipMemsetAsync(dst.rstart, 0, (P + 1) * sizeof(u64), st);
-        if (e != hipSuccess) return e;
+        if (n <= 0) {
+            e = hipMemsetAsync(dst.rstart, 0, (P + 1) * sizeof(u64), st);
+            if (e == hipSuccess) e = hipMemsetAsync(ws.rcur, 0, (P + 1) * sizeof(u64), st);
+            if (e != hipSuccess) return e;
+        }
         // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
         if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
         const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
         hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
                            (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, dst.rstart, (int)P);
         scan_u64(dst.rstart, P + 1, ws.scan_sums, st);
-        e = hipMemcpyAsync(ws.rcur, dst.rstart, P * sizeof(u64), hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass], ws.rcur,
-                           dst.runs, (int)P);
+                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass],
+                           (const u64 *)dst.rstart, ws.rcur, dst.runs, (int)P);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         prev = &dst;
