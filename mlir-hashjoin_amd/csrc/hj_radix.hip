@@ -920,6 +920,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     T sv_[SI], rv_[RI];
     unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
     u64 er[RI], es[SI];
+    bool dup_sent = false;   // this workgroup has set a.dup_flag
     ItemDesc it = a.desc[w];
     ents(a.r_runs, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
     ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
@@ -993,8 +994,13 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             if (dup) s_dup = 1u;
             __syncthreads();
             const bool unique = s_dup == 0u;
-            if (!unique && threadIdx.x == 0)
-                __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // once per workgroup: every table with a repeated key storing to
+            // the one flag serialised those stores at the memory side (C1-ref
+            // at 2^28: +3.5 ms, micro/join_micro.hip mode 1)
+            if (!unique && !dup_sent) {
+                if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dup_sent = true;
+            }
 
             // ---- probe the chunk, one sub-chunk of S rows at a time
             for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {

@@ -7,6 +7,7 @@
 #include "../csrc/hj_radix.hip"
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
@@ -19,12 +20,20 @@ __device__ u64 mixd(u64 z) {
     return z ^ (z >> 31);
 }
 
-__global__ void k_gen(ulonglong2 *r, ulonglong2 *s, u64 n) {
+// mode 0: PK-FK (every S row matches once); 1: keys uniform in [1, 2^32]
+// on both sides (C1-ref's distribution scaled to 2^28 rows: repeated build
+// keys, 1/16 of the probes match); 2: PK-FK with 1/16 of the probes matching
+__global__ void k_gen(ulonglong2 *r, ulonglong2 *s, u64 n, int mode) {
     u64 i = (u64)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
+    if (mode == 1) {
+        r[i] = make_ulonglong2((mixd(i) & 0xFFFFFFFFull) + 1, i);
+        s[i] = make_ulonglong2((mixd(i ^ 0x5555555555ull) & 0xFFFFFFFFull) + 1, i);
+        return;
+    }
     r[i] = make_ulonglong2(mixd(i), i);
     const u64 j = mixd(i ^ 0xabcdef) % n;
-    s[i] = make_ulonglong2(mixd(j), i);
+    s[i] = make_ulonglong2(mode == 2 && (mixd(i ^ 0x777) & 15) ? mixd(j + n) : mixd(j), i);
 }
 
 template <typename T>
@@ -47,10 +56,11 @@ BucketSet make_set(RadixNeed nd, int P) {
     return b;
 }
 
-int main() {
+int main(int argc, char **argv) {
+    const int mode = argc > 1 ? atoi(argv[1]) : 0;
     const u64 n = 1ull << 28;
     ulonglong2 *r = dalloc<ulonglong2>(n), *s = dalloc<ulonglong2>(n);
-    hipLaunchKernelGGL(k_gen, dim3(n / 256), dim3(256), 0, 0, r, s, n);
+    hipLaunchKernelGGL(k_gen, dim3(n / 256), dim3(256), 0, 0, r, s, n, mode);
     const RadixPlan pl = radix_plan((long long)n);
     const int P = 1 << pl.total_bits;
     printf("plan: %d passes, bits %d/%d/%d, P=%d\n", pl.passes, pl.bits[0], pl.bits[1], pl.bits[2], P);
