@@ -1251,11 +1251,359 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
     }
 }
 
+// --------------------------------------------------------------- bucketized join
+// k_join2: the same work items as k_join, but the partition's LDS table is
+// BUCKETIZED and holds no keys:
+//
+//   trow[RCAP]   the round's build rows, row j at index j (16 B wide / 8 B narrow)
+//   tslot[NB]    NB buckets of 4 u32 slots (16 B); slot = fp << 16 | j, EMPTY = ~0
+//   bcnt[NB]     bucket fill counters
+//
+// with bucket = the hash bits right below the partition bits and fp = 16
+// other hash bits (0xFFFF mapped to 0xFFFE, so no real slot equals EMPTY).
+// Build: one LDS atomicAdd per row takes a rank in its bucket (a full
+// bucket sends the row on to the next one, rarely); no CAS loops.  Probe:
+// one 16-B read of the home bucket (ds_read_b128), fingerprint compare of
+// its 4 slots, one read of the candidate row to confirm the key and fetch
+// its payload; only when the bucket is full (~2 % at load factor 0.25) does
+// the probe continue into the next bucket.  The linear-probing table of
+// k_join made every wave wait for the longest of its 64 x 5 chains (6.4
+// extra slots on average at load factor 0.5).
+//
+// Any number of matches per probe row is handled: a sub-chunk whose rows
+// match at most once each is written by ballot compaction (the R payload is
+// already in registers from the confirming read); otherwise every thread
+// re-walks its matching rows' buckets and writes the pairs at its prefix.
+// Keys are compared in full, so INT64_MIN needs no side path here.
+// ABL (diagnostics, micro/join_micro.hip): 1 no cursor atomic, 2 no writes,
+// 4 no probe, 8 no build.
+constexpr int kJ2NT = 512;   // threads per workgroup (2 workgroups per CU at 76 KiB of LDS)
+constexpr int kJ2RI = 5;     // build rows per thread per round: RCAP 2560 (a 2^28-row C3 partition peaks near 2350)
+constexpr int kJ2NBL = 11;   // 2048 buckets x 4 slots: load factor 0.25 at 2048 rows (a full bucket is rare)
+constexpr int kJ2SI = 3;     // S rows per thread per sub-chunk (5 spills: 10.1 ms; 3: 4.96 ms; 2: 4.42 ms)
+template <bool WIDE, bool WRITE, int NT, int RI, int NBL, int SI, int ABL = 0>
+__global__ __launch_bounds__(NT, 4) void k_join2(JoinArgs a) {
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // output element
+    constexpr int NB = 1 << NBL;
+    constexpr unsigned kBMask = NB - 1;
+    constexpr int RCAP = NT * RI;                 // build rows per round
+    constexpr int SUBR = NT * SI;                 // probe rows per sub-chunk
+    constexpr unsigned rb = (unsigned)RCAP >> kRunLog;
+    constexpr unsigned subb = (unsigned)SUBR >> kRunLog;
+    constexpr unsigned chb = (unsigned)kJoinSub * subb;
+    static_assert((rb << kRunLog) == RCAP && (subb << kRunLog) == SUBR, "rounds must be whole runs");
+    static_assert(RCAP < 4 * NB && RCAP < 0xFFFF, "round must fit the slots and the 16-bit row index");
+    constexpr unsigned kE = 0xFFFFFFFFu;          // EMPTY slot
+    constexpr int NW = NT / 64;
+    __shared__ T trow[RCAP];
+    __shared__ uint4 tslot[NB];                   // bucket b = 4 slots
+    __shared__ unsigned bcnt[NB / 2];             // bucket b's fill in the 16-bit half b & 1 (<= RCAP: no carry)
+    __shared__ u64 wsum[16];
+    __shared__ u64 s_base;
+    __shared__ unsigned s_cw[SI * NW];
+
+    const unsigned total = a.work_start[a.P];
+    unsigned w = blockIdx.x;
+    if (w >= total) return;
+    const T *rrows = (const T *)a.r;
+    const T *srows = (const T *)a.s;
+    PT *orr = (PT *)a.out_r;
+    PT *oss = (PT *)a.out_s;
+    const int tshift = a.tshift;
+    // rank of one more row in bucket b
+    auto take = [&](unsigned b) -> unsigned {
+        return (atomicAdd(&bcnt[b >> 1], (b & 1u) ? 0x10000u : 1u) >> ((b & 1u) * 16u)) & 0xFFFFu;
+    };
+    auto bucket_of = [&](u64 h) -> unsigned { return (unsigned)(h >> tshift) & kBMask; };
+    auto fp_of = [&](u64 h) -> unsigned {
+        const unsigned f = (unsigned)(h >> 16) & 0xFFFFu;
+        return f == 0xFFFFu ? 0xFFFEu : f;
+    };
+    // candidate slots of bucket q for fingerprint f (bit j = slot j)
+    auto cands = [&](const uint4 &q, unsigned f) -> unsigned {
+        return ((q.x >> 16) == f ? 1u : 0u) | ((q.y >> 16) == f ? 2u : 0u) | ((q.z >> 16) == f ? 4u : 0u) |
+               ((q.w >> 16) == f ? 8u : 0u);
+    };
+    auto slot_at = [&](const uint4 &q, unsigned j) -> unsigned {
+        return j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
+    };
+
+    constexpr unsigned G = NT >> kRunLog;
+    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
+    const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const u64 li = lo + (u64)i * G + wv0;
+            e[i] = li < hi ? list[li] : 0ull;
+        }
+    };
+    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
+        unsigned ok = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            if (off < (unsigned)(e[i] & 127u)) {
+                v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + off);
+                ok |= 1u << i;
+            } else {
+                v[i] = R::zero();
+            }
+        }
+        return ok;
+    };
+    T sv_[SI], rv_[RI];
+    unsigned rok = 0, sok = 0;
+    u64 er[RI], es[SI];
+    bool dup_sent = false;
+    ItemDesc it = a.desc[w];
+    ents(a.r_runs, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
+    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    ItemDesc nx = a.desc[w + gridDim.x < total ? w + gridDim.x : w];
+    auto load_r = [&](u64 r0) {
+        ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
+        return rows_of(rrows, er, rv_, RI);
+    };
+    auto load_s = [&](u64 s0) {
+        ents(a.s_runs, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
+        return rows_of(srows, es, sv_, SI);
+    };
+    while (true) {
+        rok = rows_of(rrows, er, rv_, RI);
+        sok = rows_of(srows, es, sv_, SI);
+        const bool more = w + gridDim.x < total;
+        u64 ner[RI], nes[SI];
+        ItemDesc nnx = nx;
+        if (more) {
+            ents(a.r_runs, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
+            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+            if (w + 2 * gridDim.x < total) nnx = a.desc[w + 2 * gridDim.x];
+        }
+        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
+            if (r0 != it.r_lo) rok = load_r(r0);   // later rounds (oversized partitions)
+            // ---- init: every slot EMPTY, every counter 0
+            for (int j = threadIdx.x; j < NB; j += NT) tslot[j] = make_uint4(kE, kE, kE, kE);
+            for (int j = threadIdx.x; j < NB / 2; j += NT) bcnt[j] = 0u;
+            __syncthreads();
+            // ---- build: rows into trow, one rank atomic per row (all issued
+            // before any result is used)
+            {
+                unsigned rk[RI], hb[RI];
+#pragma unroll
+                for (int i = 0; i < RI; ++i) {
+                    const bool act = ((rok >> i) & 1u) && (ABL & 8) == 0;
+                    hb[i] = bucket_of(rhash(R::key(rv_[i])));
+                    if (act) trow[i * NT + threadIdx.x] = rv_[i];
+                    rk[i] = act ? take(hb[i]) : kE;
+                }
+#pragma unroll
+                for (int i = 0; i < RI; ++i) {
+                    if (rk[i] == kE) continue;
+                    unsigned b = hb[i], r = rk[i];
+                    while (r >= 4u) {   // full: on to the next bucket
+                        b = (b + 1) & kBMask;
+                        r = take(b);
+                    }
+                    ((unsigned *)tslot)[b * 4 + r] =
+                        (fp_of(rhash(R::key(rv_[i]))) << 16) | (unsigned)(i * NT + threadIdx.x);
+                }
+            }
+            __syncthreads();
+
+            // ---- probe the chunk, one sub-chunk of S rows at a time
+            for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+                if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
+                // per row slot: st = count of confirmed build rows << 16 | the
+                // first one's index in trow; bi = the bucket read last
+                unsigned st[SI], bi[SI];
+                unsigned walk = 0u;   // bit i: row slot i's last bucket was full (walk on)
+                {
+                    uint4 q[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        bi[i] = bucket_of(rhash(R::key(sv_[i])));
+                        q[i] = ((sok >> i) & 1u) && (ABL & 4) == 0 ? tslot[bi[i]] : make_uint4(kE, kE, kE, kE);
+                    }
+                    // first candidate of every row: confirming key reads in flight together
+                    unsigned pk[SI];
+                    u64 mk[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const unsigned c = cands(q[i], fp_of(rhash(R::key(sv_[i]))));
+                        if (q[i].w != kE) walk |= 1u << i;
+                        const unsigned j = c ? (unsigned)__builtin_ctz(c) : 0u;
+                        pk[i] = c ? ((slot_at(q[i], j) & 0xFFFFu) | ((c & (c - 1u)) << 16)) : kE;
+                        mk[i] = c ? R::key(trow[slot_at(q[i], j) & 0xFFFFu]) : 0ull;
+                    }
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 key = R::key(sv_[i]);
+                        const bool first = pk[i] != kE && mk[i] == key;
+                        st[i] = first ? ((1u << 16) | (pk[i] & 0xFFFFu)) : 0u;
+                        unsigned rest = pk[i] != kE ? pk[i] >> 16 : 0u;
+                        if (rest) {   // fingerprint twins / repeated build keys: rare
+                            const uint4 qq = tslot[bi[i]];   // (re-read: q is dead by now)
+                            while (rest) {
+                                const unsigned j = __builtin_ctz(rest);
+                                rest &= rest - 1u;
+                                const unsigned x = slot_at(qq, j) & 0xFFFFu;
+                                if (R::key(trow[x]) == key) st[i] = st[i] ? st[i] + (1u << 16) : ((1u << 16) | x);
+                            }
+                        }
+                    }
+                }
+                // rows whose bucket was full walk on, all row slots in one
+                // loop (one LDS round trip per step for the whole wave)
+                while (walk) {
+                    uint4 q[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if ((walk >> i) & 1u) {
+                            bi[i] = (bi[i] + 1) & kBMask;
+                            q[i] = tslot[bi[i]];
+                        }
+                    }
+                    unsigned nw = 0u;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if (!((walk >> i) & 1u)) continue;
+                        const u64 key = R::key(sv_[i]);
+                        unsigned c = cands(q[i], fp_of(rhash(key)));
+                        while (c) {
+                            const unsigned j = __builtin_ctz(c);
+                            c &= c - 1u;
+                            const unsigned x = slot_at(q[i], j) & 0xFFFFu;
+                            if (R::key(trow[x]) == key) st[i] = st[i] ? st[i] + (1u << 16) : ((1u << 16) | x);
+                        }
+                        if (q[i].w != kE) nw |= 1u << i;
+                    }
+                    walk = nw;
+                }
+                u64 cnt = 0;
+                unsigned maxc = 0;
+#pragma unroll
+                for (int i = 0; i < SI; ++i) {
+                    const unsigned c = st[i] >> 16;
+                    cnt += c;
+                    maxc = c > maxc ? c : maxc;
+                }
+                // one rule for the whole workgroup: ballot path iff no row matched twice
+                const bool multi = __syncthreads_or(maxc > 1u ? 1 : 0) != 0;
+                if (multi && !dup_sent) {
+                    if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    dup_sent = true;
+                }
+                if (WRITE && !multi) {
+                    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+                    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+                    unsigned lpre[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 bal = __ballot(st[i] != 0u);
+                        lpre[i] = (unsigned)__popcll(bal & lt);
+                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                    }
+                    __syncthreads();
+                    if (wv == 0) {   // exclusive scan of the SI * NW run lengths
+                        constexpr int K = (SI * NW + 63) / 64;
+                        unsigned v[K], sum = 0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int j = lane * K + k;
+                            v[k] = j < SI * NW ? s_cw[j] : 0u;
+                            sum += v[k];
+                        }
+                        unsigned x = sum;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const unsigned y = __shfl_up(x, o, 64);
+                            if (lane >= o) x += y;
+                        }
+                        unsigned run = x - sum;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int j = lane * K + k;
+                            if (j < SI * NW) s_cw[j] = run;
+                            run += v[k];
+                        }
+                        if (lane == 63 && x)
+                            s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, (u64)x);
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if constexpr ((ABL & 2) != 0) break;
+                        if (!st[i]) continue;
+                        const u64 pos = s_base + s_cw[i * NW + wv] + lpre[i];
+                        if (pos < (u64)a.cap) {
+                            st_s<kNtJoinSt>(orr + pos, (PT)R::pay(trow[st[i] & 0xFFFFu]));
+                            st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
+                        }
+                    }
+                    __syncthreads();   // s_cw / s_base reused by the next sub-chunk
+                    continue;
+                }
+                u64 tot;
+                const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
+                if constexpr (!WRITE) {
+                    if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                } else if (tot) {
+                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, tot);
+                    __syncthreads();
+                    u64 pos = s_base + pre;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if constexpr ((ABL & 2) != 0) break;
+                        if (!st[i]) continue;
+                        const u64 key = R::key(sv_[i]);
+                        const PT spay = (PT)R::pay(sv_[i]);
+                        const u64 h = rhash(key);
+                        const unsigned f = fp_of(h);
+                        unsigned b = bucket_of(h);
+                        uint4 q;
+                        do {   // the home bucket, then on while full
+                            q = tslot[b];
+                            unsigned c = cands(q, f);
+                            while (c) {
+                                const unsigned j = __builtin_ctz(c);
+                                c &= c - 1u;
+                                const T rr = trow[slot_at(q, j) & 0xFFFFu];
+                                if (R::key(rr) != key) continue;
+                                if (pos < (u64)a.cap) {
+                                    orr[pos] = (PT)R::pay(rr);
+                                    oss[pos] = spay;
+                                }
+                                ++pos;
+                            }
+                            b = (b + 1) & kBMask;
+                        } while (q.w != kE);
+                    }
+                    __syncthreads();   // s_base reused by the next sub-chunk
+                }
+            }
+            __syncthreads();   // table reused by the next round / item
+        }
+        if (!more) break;
+        w += gridDim.x;
+        it = nx;
+        nx = nnx;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) er[i] = ner[i];
+#pragma unroll
+        for (int i = 0; i < SI; ++i) es[i] = nes[i];
+    }
+}
+
+
 // Join kernel variant: log2 LDS slots and workgroup size.  HJ_JOIN_TSL
-// (11 | 12 | 13) overrides the default for experiments.
+// (11 | 12 | 13) overrides the default for experiments.  HJ_JOIN=2 selects
+// the bucketized k_join2 (measured slower: profiles/r02_micro_join_bucketized.txt).
 struct JoinVariant {
     int tsl;
     int nt;
+    int kind;   // 1 k_join, 2 k_join2
+    int si;     // S rows per thread per sub-chunk
 };
 JoinVariant join_variant() {
     static int tsl = [] {
@@ -1263,7 +1611,12 @@ JoinVariant join_variant() {
         const int v = e ? atoi(e) : 12;
         return (v == 11 || v == 12 || v == 13) ? v : 12;
     }();
-    return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256)};
+    static int kind = [] {
+        const char *e = getenv("HJ_JOIN");
+        return (e && atoi(e) == 2) ? 2 : 1;
+    }();
+    if (kind == 2) return JoinVariant{12, 512, 2, kJ2SI};
+    return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256), 1, kJoinItems};
 }
 
 int cu_count() {
@@ -1372,7 +1725,7 @@ size_t exclusive_scan_sums(unsigned long long len) { return (size_t)(len / kScan
 
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs) {
     const JoinVariant jv = join_variant();
-    const u64 chr = (u64)kJoinSub * (((u64)jv.nt * kJoinItems) >> kRunLog);
+    const u64 chr = (u64)kJoinSub * (((u64)jv.nt * jv.si) >> kRunLog);
     return s_runs / chr + (1ull << pl.total_bits) + 2;
 }
 
@@ -1480,12 +1833,12 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     const JoinVariant jv = join_variant();
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
     // persistent grid: as many workgroups as fit at once (LDS-limited)
-    const int per_cu = jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4);
+    const int per_cu = jv.kind == 2 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
     const unsigned pg = (unsigned)(per_cu * cu_count());
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
     // long as ~16 items per workgroup remain for balance
-    const unsigned subb = (unsigned)((jv.nt * kJoinItems) >> kRunLog);
+    const unsigned subb = (unsigned)((jv.nt * jv.si) >> kRunLog);
     u64 chb = (u64)kJoinSub * subb;
     const u64 want = (u64)s_runs / (16ull * pg);
     if (want > chb) chb = (want + subb - 1) / subb * subb;
@@ -1504,7 +1857,8 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.P = P;
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
-    a.tshift = 64 - pl.total_bits - jv.tsl;   // the hash bits right below the partition bits
+    // the hash bits right below the partition bits: LDS slot (k_join) or bucket (k_join2)
+    a.tshift = 64 - pl.total_bits - (jv.kind == 2 ? kJ2NBL : jv.tsl);
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;
@@ -1518,13 +1872,24 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         else if (jv.tsl == 12) HJ_JOIN(W, WR, 12, 512); \
         else HJ_JOIN(W, WR, 11, 256);                 \
     } while (0)
-    if (wide) {
+#define HJ_JOIN2(W, WR) \
+    hipLaunchKernelGGL((k_join2<W, WR, kJ2NT, kJ2RI, kJ2NBL, kJ2SI>), dim3(grid), dim3(kJ2NT), 0, st, a)
+    if (jv.kind == 2) {
+        if (wide) {
+            if (count_only) HJ_JOIN2(true, false);
+            else HJ_JOIN2(true, true);
+        } else {
+            if (count_only) HJ_JOIN2(false, false);
+            else HJ_JOIN2(false, true);
+        }
+    } else if (wide) {
         if (count_only) HJ_JOIN_V(true, false);
         else HJ_JOIN_V(true, true);
     } else {
         if (count_only) HJ_JOIN_V(false, false);
         else HJ_JOIN_V(false, true);
     }
+#undef HJ_JOIN2
 #undef HJ_JOIN_V
 #undef HJ_JOIN
     return hipGetLastError();

@@ -149,6 +149,19 @@ int main(int argc, char **argv) {
         a.tshift = 64 - pl.total_bits - TSL;                                                              \
         hipLaunchKernelGGL((k_join<true, WR, TSL, NT, ABL>), dim3(PER_CU * cus), dim3(NT), 0, 0, a);      \
     })
+#define J2(WR, ABL, SI, NAME)                                                                               \
+    run(NAME, [&] {                                                                                       \
+        a.tshift = 64 - pl.total_bits - kJ2NBL;                                                           \
+        hipLaunchKernelGGL((k_join2<true, WR, kJ2NT, kJ2RI, kJ2NBL, SI, ABL>), dim3(2 * cus), dim3(kJ2NT), 0, 0, a); \
+    })
+    J2(true, 0, 5, "k_join2 SI5 full");
+    J2(false, 0, 5, "k_join2 SI5 count only");
+    J2(true, 3, 5, "k_join2 SI5 no atomic, no writes");
+    J2(true, 0, 3, "k_join2 SI3 full");
+    J2(false, 0, 3, "k_join2 SI3 count only");
+    J2(true, 0, 2, "k_join2 SI2 full");
+    J2(false, 0, 2, "k_join2 SI2 count only");
+    J2(true, 3, 2, "k_join2 SI2 no atomic, no writes");
     J(12, 512, 2, true, 0, "full");
     J(12, 512, 2, false, 0, "count only");
     J(12, 512, 2, true, 1, "no atomic");
