@@ -6,18 +6,25 @@ int64 payload, PK-FK synthetic relations (SURVEY 8(d) C3 shape: R keys
 unique, every S row matches exactly one R row).  One step = one complete
 join of the whole relations with inputs resident in HBM:
 
-  N = 1 : table init + build + probe (one GPU holds everything: ~22 GiB)
-  N > 1 : radix partition R and S -> RCCL all-to-all of 16-B tuples ->
-          local init + build + probe (strong scaling: the GLOBAL relations
-          stay 2^28 x 2^28; each rank generates its 1/N slice)
+  N = 1 : build (R radix partition) + probe (S radix partition + LDS join)
+  N > 1 : radix-route R and S -> RCCL all-to-all of 16-B tuples -> local
+          build + probe (strong scaling: the GLOBAL relations stay
+          2^28 x 2^28; each rank generates its 1/N slice).  Build sides of
+          <= 2^21 rows are all-gathered instead (no S shuffle).
 
 value = |S| / (time per step), the whole job over all ranks (max over ranks).
-Launch:  python bench.py [--gpus 1 --steps K --warmup W]
+`roofline` is SURVEY 8(d)'s probe-phase figure: 48 B per probe tuple (16 B S
+row + 16 B slot + 16 B output pair) over the probe phase's HIP-event time;
+`roofline.kernel` is the same for the dominant kernel (k_join) alone.
+Launch:  python bench.py [--gpus 1 --steps K --warmup W --config C3]
          python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -28,15 +35,28 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_ACHIEVABLE_GBS = 6290.0   # same guide: float4 copy, measured
 
 CONFIGS = {
-    # name: (log2 |R|, log2 |S|, distribution, description)
-    "C3": (28, 28, "pkfk", "PK-FK |R|=|S|=2^28 int64 key+payload, match fraction 1"),
-    "C1": (26, 26, "pkfk", "PK-FK |R|=|S|=2^26 int64 key+payload, match fraction 1"),
-    "C1-ref": (26, 26, "uniform", "uniform keys in [1,2^30] both sides, |R|=|S|=2^26 int64"),
-    "C2": (20, 30, "pkfk", "PK-FK |R|=2^20 build, |S|=2^30 probe, int64"),
-    "C4": (28, 28, "zipf", "PK build |R|=2^28, Zipf(0.9) foreign keys |S|=2^28, int64"),
+    # name: (|R|, |S|, distribution, key type, description)
+    "C3": (1 << 28, 1 << 28, "pkfk", "int64", "PK-FK |R|=|S|=2^28 int64 key+payload, match fraction 1"),
+    "C1": (1 << 26, 1 << 26, "pkfk", "int64", "PK-FK |R|=|S|=2^26 int64 key+payload, match fraction 1"),
+    "C1-ref": (1 << 26, 1 << 26, "uniform30", "int64", "uniform keys in [1,2^30] both sides, |R|=|S|=2^26 int64"),
+    "C2": (1 << 20, 1 << 30, "pkfk", "int64", "PK-FK |R|=2^20 build, |S|=2^30 probe, int64"),
+    "C4": (1 << 28, 1 << 28, "zipf", "int64", "PK build |R|=2^28, Zipf(0.9) foreign keys |S|=2^28, int64"),
+    # the reference's own published workloads (join-performances.md:3-6 / :16-19 and :8-11 / :21-24),
+    # in its types: i32 keys, row-id payloads, (rowR, rowS) i32 output
+    "REF-A": (10_000_000, 10_000_000, "ref100k", "int32",
+              "reference workload 1: 10M x 10M i32 keys uniform in [1, 100k] (~1e9 result rows)"),
+    "REF-B": (100_000_000, 100_000_000, "ref1e9", "int32",
+              "reference workload 2: 100M x 100M i32 keys uniform in [1, 1e9] (~1e7 result rows)"),
 }
+# the reference's own times for those workloads (join-performances.md; sm_86, all four kernels + module loads)
+REFERENCE_PUBLISHED = {
+    "REF-A": {"join_v1_s": 2.0, "join_v2_s": 1.5, "source": "join-performances.md:3-6, :16-19"},
+    "REF-B": {"join_v1_s": 12.0, "join_v2_s": 12.5, "source": "join-performances.md:8-11, :21-24"},
+}
+PROBE_KERNELS = ("k_pass", "k_join")   # probe phase: S partition passes + the LDS join
 
 
 def parse():
@@ -48,6 +68,7 @@ def parse():
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=22)
+    ap.add_argument("--no-host-leg", action="store_true", help="skip the host-memref (PCIe-inclusive) leg")
     ap.add_argument("--verify", action="store_true", help="check the last step's output properties")
     ap.add_argument("--strategy", default="auto", choices=["auto", "global", "radix"])
     ap.add_argument("--radix-bits", type=int, default=0)
@@ -56,38 +77,179 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seed, log2n, threads):
-    """The reference's join_v2 (chained table, key urem H with H = |R|/100 as
-    join-performances.md:3,8, count -> block scan -> staged probe) restated on
-    host threads (oracle/, test infrastructure), timed on a bounded sample."""
+# ---------------------------------------------------------------- CPU baseline
+def host_facts():
+    """Cores this process may use on the host (affinity and cgroup quota) and
+    the CPU model, as SURVEY 8(d) asks the CPU baseline to state."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = platform.processor() or ""
+    try:
+        for line in subprocess.check_output(["lscpu"], text=True, timeout=10).splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    usable = min(aff, quota) if quota else aff
+    return {"nproc": aff, "cpu_count": os.cpu_count(), "cgroup_cpus": quota, "usable_cores": usable,
+            "lscpu_model": model}
+
+
+def cpu_baseline(seed, log2n):
+    """The reference's algorithms restated on the host (oracle/hj_oracle.c,
+    test infrastructure), each timed on a bounded sample:
+      * join_v2 (join_v2.mlir:227-604: chained table, key urem H, count ->
+        block scan -> staged probe) at H = |R|/100 (the reference's ratio,
+        join-performances.md:3,8) and H = |R|, on all usable cores and on 1;
+      * the nested loop (shared.cpp:154-165, nested-loop.mlir:29-192) up to
+        2^16 x 2^16, extrapolated quadratically to 2^28 x 2^28 (labelled)."""
     sys.path.insert(0, ROOT)
     from oracle import pyoracle as O
-    n = 1 << log2n
-    rk, rp, sk, sp = O.gen_pkfk_i64(seed, n, n)
-    H = max(1, n // 100)
-    O.chained_join_i64_omp(rk[:4096], rp[:4096], sk[:4096], sp[:4096], 41, threads)   # warm the pool
-    t0 = time.perf_counter()
-    m, ph = O.chained_join_i64_omp(rk, rp, sk, sp, H, threads)
-    dt = time.perf_counter() - t0
-    assert m == n, (m, n)
-    return {"value": n / dt, "unit": "probe tuples/s", "cores": threads, "kind": "port",
-            "sample": f"|R|=|S|=2^{log2n} PK-FK int64, H=|R|/100 (reference ratio), join_v2 restated "
-                      f"(oracle/hj_oracle.c) on {threads} host threads; {dt:.2f} s "
-                      f"(init {ph[0]:.2f} / build {ph[1]:.2f} / count {ph[2]:.2f} / probe {ph[3]:.2f} s)"}
+    facts = host_facts()
+    allc = facts["usable_cores"]
+    runs = []
+
+    def v2(log2, H_div, threads):
+        n = 1 << log2
+        rk, rp, sk, sp = O.gen_pkfk_i64(seed, n, n)
+        H = max(1, n // H_div)
+        O.chained_join_i64_omp(rk[:4096], rp[:4096], sk[:4096], sp[:4096], 41, threads)   # warm the pool
+        t0 = time.perf_counter()
+        m, ph = O.chained_join_i64_omp(rk, rp, sk, sp, H, threads)
+        dt = time.perf_counter() - t0
+        assert m == n, (m, n)
+        probe_s = ph[2] + ph[3]
+        runs.append({"algorithm": "join_v2 restated", "H": f"|R|/{H_div}" if H_div > 1 else "|R|",
+                     "rows": f"2^{log2} x 2^{log2}", "threads": threads, "seconds": round(dt, 3),
+                     "probe_tuples_per_s": round(n / probe_s, 1) if probe_s > 0 else None,
+                     "joined_rows_per_s": round(m / dt, 1),
+                     "phases_s": {"init": round(ph[0], 4), "build": round(ph[1], 4), "count": round(ph[2], 4),
+                                  "probe": round(ph[3], 4)}})
+        return runs[-1]
+
+    def nested(log2, threads):
+        n = 1 << log2
+        rk, _, sk, _ = O.gen_pkfk_i64(seed, n, n)
+        L = O.lib()
+        t0 = time.perf_counter()
+        m = L.oracle_nested_loop_count_i64_omp(rk.ctypes.data, n, sk.ctypes.data, n, threads)
+        dt = time.perf_counter() - t0
+        assert m == n, (m, n)
+        ext = dt * (2.0 ** (28 - log2)) ** 2
+        runs.append({"algorithm": "nested loop restated", "rows": f"2^{log2} x 2^{log2}", "threads": threads,
+                     "seconds": round(dt, 3), "probe_tuples_per_s": round(n / dt, 1),
+                     "extrapolated_2p28": {"seconds": round(ext, 1), "probe_tuples_per_s": round((1 << 28) / ext, 2),
+                                           "note": "quadratic extrapolation from the measured sample, not measured"}})
+        return runs[-1]
+
+    head = v2(log2n, 100, allc)                      # the headline: reference ratio, all cores
+    v2(max(16, log2n - 2), 100, 1)                   # 1 core (bounded sample)
+    v2(log2n, 1, allc)                               # H = |R|
+    v2(log2n, 1, 1)
+    nested(17, allc)
+    nested(16, 1)
+    return {"value": head["probe_tuples_per_s"], "unit": "probe tuples/s", "cores": allc, "kind": "port",
+            "sample": f"join_v2 restated (oracle/hj_oracle.c), |R|=|S|=2^{log2n} PK-FK int64, H=|R|/100 "
+                      f"(reference ratio), {allc} host threads; probe = count + probe phases "
+                      f"({head['phases_s']['count'] + head['phases_s']['probe']:.2f} s)",
+            "host": facts, "runs": runs}
 
 
-def pmc_traffic(config, n_gpus, kernel):
-    """HBM bytes per launch of `kernel` for this workload from the committed
-    rocprofv3 PMC summary (profiles/pmc_latest.json, written by
-    profiles/pmc_to_json.py), or None."""
+# ---------------------------------------------------------------- roofline helpers
+def kernel_source_sha():
+    h = hashlib.sha256()
+    for f in ("hj_radix.hip", "hj_kernels.hip"):
+        with open(os.path.join(ROOT, "mlir-hashjoin_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_record(config, n_gpus):
+    """This workload's rocprofv3 PMC summary (profiles/pmc_latest.json, written
+    by profiles/pmc_to_json.py) if it was collected from the current kernel
+    sources, else (None, reason)."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        e = d.get(f"{config}/n{n_gpus}", {}).get("kernels", {}).get(kernel)
-        return None if e is None else e.get("hbm_bytes_per_launch")
-    except (OSError, ValueError, AttributeError):
+    except (OSError, ValueError):
+        return None, "no profiles/pmc_latest.json"
+    e = d.get(f"{config}/n{n_gpus}")
+    if not e:
+        return None, f"no PMC record for {config}/n{n_gpus}"
+    if e.get("source_sha") != kernel_source_sha():
+        return None, f"stale: PMC of kernel sources {e.get('source_sha')} (now {kernel_source_sha()})"
+    return e, f"rocprofv3 PMC, {e.get('source', '')}"
+
+
+def traffic_of(rec, names):
+    """HBM bytes per launch summed over the probe phase's kernels."""
+    if not rec:
         return None
+    ks = rec.get("kernels", {})
+    tot = 0
+    for base in names:
+        k = ks.get(base)
+        if not k:
+            return None
+        if base == "k_pass":
+            # the S side runs each k_pass variant once: sum the variants' averages
+            tot += sum(v["hbm_bytes_per_launch"] for v in k["variants"].values())
+        else:
+            tot += k["hbm_bytes_per_launch"]
+    return int(tot)
+
+
+# ---------------------------------------------------------------- main
+def gen_inputs(hashjoin, a, NR, NS, distn, r0, nr, s0, ns):
+    if distn == "pkfk":
+        return hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, ns)
+    if distn == "zipf":
+        rk, rp, _, _ = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, 0)
+        sk, sp = hashjoin.gen_zipf(a.seed, NR, NS, 0.9, s0, ns)
+        return rk, rp, sk, sp
+    if distn == "uniform30":
+        rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)
+        sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 1 << 30, ns, i0=s0)
+        return rk, rp, sk, sp
+    hi = 100_000 if distn == "ref100k" else 1_000_000_000
+    return (hashjoin.gen_uniform_i32(a.seed, 1, 1, hi, nr, i0=r0), None,
+            hashjoin.gen_uniform_i32(a.seed, 2, 1, hi, ns, i0=s0), None)
+
+
+def expected_rows(distn, NR, NS):
+    return NS if distn in ("pkfk", "zipf") else None
+
+
+def host_leg(hashjoin, seed):
+    """The literal drop-in: hj_count_i64 -> hj_probe_i64 over HOST memrefs
+    (run_test.sh's call shape), PCIe included, 2^24 x 2^24 PK-FK int64."""
+    import numpy as np
+    from hashjoin import memref as MR
+    n = 1 << 24
+    rk, rp, sk, sp = (t.cpu().numpy() for t in hashjoin.gen_pkfk(seed, n, n))
+    MR.count_i64(rk[:1024], rp[:1024], sk[:1024], sp[:1024])   # warm
+    h0 = hashjoin.lib.hj_host_memo_hits()
+    t0 = time.perf_counter()
+    m = MR.count_i64(rk, rp, sk, sp)
+    t1 = time.perf_counter()
+    o_r = np.empty(m, np.int64)
+    o_s = np.empty(m, np.int64)
+    rc = MR.probe_i64(rk, rp, sk, sp, o_r, o_s)
+    t2 = time.perf_counter()
+    assert rc == 0 and m == n
+    return {"api": "hj_count_i64 -> hj_probe_i64 (host memrefs, PCIe Gen5 included)", "rows": "2^24 x 2^24",
+            "count_ms": round((t1 - t0) * 1e3, 2), "probe_ms": round((t2 - t1) * 1e3, 2),
+            "probe_reused_count_join": hashjoin.lib.hj_host_memo_hits() == h0 + 1,
+            "probe_tuples_per_s_end_to_end": round(n / (t2 - t0), 1),
+            "pcie_payload_bytes": n * 32 * 2 + m * 16}
 
 
 def main():
@@ -107,35 +269,36 @@ def main():
     import hashjoin
     from hashjoin.dist import distributed_join
 
-    lr, ls, distn, desc = CONFIGS[a.config]
-    NR, NS = 1 << lr, 1 << ls
+    NR, NS, distn, ktype, desc = CONFIGS[a.config]
+    wide = ktype == "int64"
+    if use_dist and not wide:
+        raise SystemExit("the multi-GPU path joins int64 key/payload columns")
     r0, nr = rank * NR // world, (rank + 1) * NR // world - rank * NR // world
     s0, ns = rank * NS // world, (rank + 1) * NS // world - rank * NS // world
-    if distn == "pkfk":
-        rk, rp, sk, sp = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, ns)
-    elif distn == "zipf":
-        rk, rp, _, _ = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, 0)
-        sk, sp = hashjoin.gen_zipf(a.seed, NR, NS, 0.9, s0, ns)
-    else:
-        rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)
-        sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 1 << 30, ns, i0=s0)
+    rk, rp, sk, sp = gen_inputs(hashjoin, a, NR, NS, distn, r0, nr, s0, ns)
     hj = hashjoin.HashJoin(local)
     hj.set_strategy(a.strategy, radix_bits=a.radix_bits)
-    expect_m = NS if distn in ("pkfk", "zipf") else None
+    expect_m = expected_rows(distn, NR, NS)
     torch.cuda.synchronize()
 
-    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0, "route": 0.0,
-              "partition+exchange": 0.0}
+    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0, "route": 0.0}
     last = {}
 
     if not use_dist:
-        hj.allocate_hash_table(NR, 64)
+        hj.allocate_hash_table(NR, 64 if wide else 32)
         hj.build_table(rk, rp)
-        hj.reserve_probe(NS, 64)
-        cap = NS if distn in ("pkfk", "zipf") else int(NR * NS / (1 << 30) * 1.1) + 4096
-        out_r = torch.empty(cap, dtype=torch.int64, device="cuda")
-        out_s = torch.empty_like(out_r)
+        hj.reserve_probe(NS, 64 if wide else 32)
+        odt = torch.int64 if wide else torch.int32
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        # size the output once: the exact M (a count) for the duplicate-heavy
+        # workloads, |S| for the key joins
+        if expect_m is None:
+            hj.probe_relation(sk, sp, None, None, count=cnt)
+            cap = int(cnt.item())
+        else:
+            cap = NS
+        out_r = torch.empty(max(cap, 1), dtype=odt, device="cuda")
+        out_s = torch.empty_like(out_r)
         hj.set_timing(True)
 
         def step(acc):
@@ -162,7 +325,7 @@ def main():
                 phases["probe"] += ev["built"].elapsed_time(ev["probed"])
             last["m"] = o_r.numel()
             last["rows"] = ev["rows"]
-            last["out"] = (o_r, o_s)
+            last["mode"] = ev["mode"]
 
     for _ in range(a.warmup):
         step(False)
@@ -178,47 +341,73 @@ def main():
     elapsed = time.perf_counter() - t0
 
     m_local = last["m"]
+    per_rank = None
     if use_dist:
-        tt = torch.tensor([elapsed, float(m_local)], dtype=torch.float64, device="cuda")
-        mx = tt.clone(); dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt.clone(); dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx[0].item()); m_total = int(sm[1].item())
+        mine = torch.tensor([elapsed, float(m_local), float(last["rows"][0]), float(last["rows"][1]),
+                             phases["route"] / a.steps, phases["build"] / a.steps, phases["probe"] / a.steps],
+                            dtype=torch.float64, device="cuda")
+        allr = torch.empty(world * mine.numel(), dtype=torch.float64, device="cuda")
+        dist.all_gather_into_tensor(allr, mine)
+        allr = allr.view(world, -1).cpu().tolist()
+        elapsed = max(r[0] for r in allr)
+        m_total = int(sum(r[1] for r in allr))
+        per_rank = [{"rank": i, "result_rows": int(r[1]), "build_rows": int(r[2]), "probe_rows": int(r[3]),
+                     "route_ms": round(r[4], 4), "build_ms": round(r[5], 4), "probe_ms": round(r[6], 4),
+                     "ms_per_step": round(r[0] * 1e3 / a.steps, 4)} for i, r in enumerate(allr)]
     else:
         m_total = m_local
     if expect_m is not None and m_total != expect_m:
         raise SystemExit(f"join produced {m_total} rows, expected {expect_m}")
 
     if a.verify and not use_dist:
-        o_r, o_s = out_r[:m_local], out_s[:m_local]
+        o_r, o_s = out_r[:m_local].long(), out_s[:m_local].long()
         assert bool((rk[o_r] == sk[o_s]).all()), "non-matching pair in output"
 
     ms = elapsed * 1000.0 / a.steps
     value = NS / (ms / 1000.0)
     ph = {k: round(v / a.steps, 4) for k, v in phases.items() if v > 0}
 
-    # Roofline of the dominant kernel (DESIGN.md "Measurement").  Radix: k_join,
-    # the longest single launch; algorithmic bytes per launch = 16 B per R row
-    # + 16 B per S row read once + 16 B per output pair (= 48 B per probe row
-    # at |R| = |S|, f = 1).  Global table: k_probe, 16 B S row + 16 B slot +
-    # 16 B output per probe row.  Duration: HIP events on the
-    # launch stream around the join (probe_join phase).
+    # SURVEY 8(d) algorithmic bytes.  int64: 16 B S row + 16 B slot + 16 B
+    # output pair per probe row (48 B at f = 1); i32 (reference types): 4 B
+    # S key + 8 B slot + 8 B output pair.
+    K, SLOT, PAIR = (16, 16, 16) if wide else (4, 8, 8)
     probe_ms = phases["probe"] / a.steps
     join_ms = phases["probe_join"] / a.steps
     build_ms = (phases["init"] + phases["build"]) / a.steps
     strategy = hj.strategy_used or a.strategy
+    probe_bytes = ns * (K + SLOT) + m_local * PAIR
     if use_dist:
-        # per-kernel events are not recorded through the distributed path:
-        # the probe phase (S partition + k_join on the received tuples)
         nr_loc, ns_loc = last["rows"]
-        kern, join_ms = "probe phase (local S partition + k_join)", probe_ms
-        kbytes = (nr_loc + ns_loc) * 16 + m_local * 16
-    elif strategy == "radix":
-        kern, kbytes = "k_join", (nr + ns) * 16 + m_local * 16
-    else:
-        kern, kbytes = "k_probe", ns * 32 + m_local * 16
-    achieved = kbytes / (join_ms / 1000.0) / 1e9 if join_ms > 0 else None
-    probe_bytes = ns * 32 + m_local * 16   # 48 B per probe row at f = 1
-    passes = hj.radix_passes if strategy == "radix" else 0
+        probe_bytes = ns_loc * (K + SLOT) + m_local * PAIR
+    rec, traffic_note = pmc_record(a.config, world)
+    info = hashjoin.device_info(local)
+
+    def frac(b, t_ms, peak=HBM_PEAK_GBS):
+        return round(b / (t_ms / 1000.0) / 1e9 / peak, 4) if t_ms > 0 else None
+
+    roof = {
+        "scope": ("probe phase: S radix partition passes + k_join (SURVEY 8(d) t_probe)" if strategy == "radix"
+                  else "probe phase: k_probe + k_probe_slow (global table)"),
+        "bound": "hbm",
+        "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": frac(probe_bytes, probe_ms),
+        "traffic": traffic_of(rec, PROBE_KERNELS) if (strategy == "radix" and not use_dist) else None,
+        "traffic_source": traffic_note,
+        "algorithmic_bytes": probe_bytes,
+        "bytes_per_probe_row": round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2),
+        "ms": round(probe_ms, 4),
+        "frac_of_achievable": frac(probe_bytes, probe_ms, HBM_ACHIEVABLE_GBS),
+        "target": "north_star: frac >= 0.40 at |R|=|S|=2^28 (t_probe <= 4.0 ms)",
+    }
+    if not use_dist and strategy == "radix":
+        kbytes = (nr + ns) * (16 if wide else 8) + m_local * PAIR
+        roof["kernel"] = {"name": "k_join (hj_radix.hip)", "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
+                          if join_ms > 0 else None, "frac": frac(kbytes, join_ms),
+                          "algorithmic_bytes_per_launch": kbytes, "avg_launch_ms": round(join_ms, 4),
+                          "traffic": (rec or {}).get("kernels", {}).get("k_join", {}).get("hbm_bytes_per_launch")
+                          if rec else None}
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),
@@ -230,45 +419,39 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int64",
-        "data": "synthetic (counter-based PK-FK generator, seed 0x5EED, generated on device)",
-        "config": {"workload": f"{a.config}: {desc}", "R_rows": NR, "S_rows": NS, "key": "int64",
-                   "payload": "int64", "distribution": distn,
+        "dtype": ktype,
+        "data": f"synthetic (counter-based generator, seed {a.seed:#x}, generated on device)",
+        "config": {"workload": f"{a.config}: {desc}", "R_rows": NR, "S_rows": NS, "key": ktype,
+                   "payload": "int64" if wide else "row id (i32)", "distribution": distn,
                    "parallelism": ("single GPU" if not use_dist
-                                   else f"radix-partitioned x{world}, RCCL all-to-all")},
+                                   else f"hash-routed x{world} ({last['mode']}), RCCL")},
         "joined_rows_per_sec": round(m_total / (ms / 1000.0), 1),
         "result_rows": m_total,
         "phase_ms": ph,
         "strategy": strategy,
-        "roofline": {
-            "kernel": kern if use_dist else f"{kern} ({'hj_radix.hip' if kern == 'k_join' else 'hj_kernels.hip'})",
-            "bound": "hbm",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": pmc_traffic(a.config, world, kern),
-            "algorithmic_bytes_per_launch": kbytes,
-            "avg_launch_ms": round(join_ms, 4),
-        },
-        # the whole probe phase (S partition passes + join for radix) at
-        # SURVEY 8(d)'s 48 B per probe row
-        "probe_phase": {
-            "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
-            "frac": round(probe_bytes / (probe_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4) if probe_ms > 0 else None,
-            "unit": "GB/s", "algorithmic_bytes": probe_bytes, "ms": round(probe_ms, 4),
-        },
-        # build phase: radix = R partition passes, each reading and writing 16 B per row
+        "roofline": roof,
         "build_phase": {
-            "kernel": f"k_pass x{passes}" if strategy == "radix" else "k_init + k_build",
-            "algorithmic_bytes": nr * 32 * max(1, passes),
-            "achieved": round(nr * 32 * max(1, passes) / (build_ms / 1000.0) / 1e9, 1) if build_ms > 0 else None,
-            "unit": "GB/s", "ms": round(build_ms, 4),
+            "kernel": f"k_pass x{hj.radix_passes}" if strategy == "radix" else "k_init + k_build",
+            "algorithmic_bytes": nr * 32 * max(1, hj.radix_passes if strategy == "radix" else 1),
+            "ms": round(build_ms, 4),
         },
+        "device": {"name": torch.cuda.get_device_name(local), **info,
+                   "peak_used_gbs": HBM_PEAK_GBS,
+                   "peak_note": "8.0 TB/s spec (MI355X_MICROARCH.md); 2 x memory clock x bus width of "
+                                "hipDeviceProp is peak_mb_per_s"},
     }
+    if a.config in REFERENCE_PUBLISHED:
+        pub = REFERENCE_PUBLISHED[a.config]
+        line["reference_published"] = {**pub, "probe_tuples_per_s_join_v2": round(NS / pub["join_v2_s"], 1),
+                                       "speedup_vs_join_v2": round(value / (NS / pub["join_v2_s"]), 1),
+                                       "note": "reference on sm_86 with module loads in its timers; a "
+                                               "different GPU, not a like-for-like baseline"}
+    if per_rank is not None:
+        line["per_rank"] = per_rank
+    if rank == 0 and not use_dist and not a.no_host_leg and a.config == "C3":
+        line["host_memref"] = host_leg(hashjoin, a.seed)
     if rank == 0 and not use_dist and not a.no_cpu_baseline:
-        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-        line["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_sample_log2, threads)
+        line["cpu_baseline"] = cpu_baseline(a.seed, a.cpu_sample_log2)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:

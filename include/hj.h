@@ -59,6 +59,10 @@ typedef struct hj_ctx hj_ctx;
 
 int hj_abi_version(void);
 const char *hj_last_error(void);
+/* Device facts for the roofline: [0] CUs, [1] memory clock (kHz), [2] memory
+ * bus width (bits), [3] L2 bytes (one XCD), [4] HBM bytes, [5] shader clock
+ * (kHz), [6] LDS bytes per CU, [7] 2 x memory clock x bus width (MB/s). */
+int hj_device_info(int device, int64_t out[8]);
 
 /* ------------------------------------------------------------------ context
  * One context = one device + its hash-table workspace.  Replaces the
@@ -137,7 +141,7 @@ int hj_dev_count_i32(hj_ctx *ctx, const int32_t *skey, int64_t n, uint64_t *d_co
 int hj_dev_probe_i32(hj_ctx *ctx, const int32_t *skey, int64_t n, int64_t row_base,
                      int32_t *out_r, int32_t *out_s, int64_t out_cap, uint64_t *d_count, void *stream);
 
-/* Radix partition of rows into nparts groups by a key hash independent of
+/* Radix partition of rows into nparts (1..8192) groups by a key hash independent of
  * the table's slot hash: out_tuples (2*n int64) receives packed {key, pay}
  * tuples grouped by partition in order 0..nparts-1, d_counts (nparts uint64)
  * the group sizes.  Multi-GPU routing step (north_star: "build-side
@@ -210,10 +214,23 @@ int64_t hj_host_join_ooc_i64(hj_ctx *ctx, const int64_t *rkey, const int64_t *rp
 
 /* ------------------------------------------------------- host memref ABI
  * Two-phase, reference-shaped (mirrors @countRows -> alloc -> @probeRelation,
- * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion.  Both calls
- * are self-contained (copy in, build, probe, copy out); offset and stride of
- * every memref are honoured.  hj_probe_* returns HJ_OK, or HJ_ERR_CAPACITY
- * when the output memrefs' size differs from the join's row count. */
+ * join_v2.mlir:672-688).  Each memref is the 5-scalar expansion; offset and
+ * stride of every memref are honoured.  hj_probe_* returns HJ_OK, or
+ * HJ_ERR_CAPACITY when the output memrefs' size differs from the join's row
+ * count.
+ *
+ * Count -> probe reuse: the reference's @countRows leaves its table for
+ * @probeRelation (join_v1.mlir:110-176).  Here the count call performs the
+ * whole join and keeps the pairs on the device; a following call whose
+ * inputs are byte-identical (uploaded again and compared on the device, so
+ * a caller that changed its buffers in between gets a fresh join) returns
+ * them without building or probing again.  hj_host_memo_hits() counts
+ * those reuses.
+ *
+ * Threading: these host-memref entry points (and the ciface / rows /
+ * selection ones below) use one default context per device; each call holds
+ * that context's lock, so concurrent callers are serialised, never mixed. */
+int64_t hj_host_memo_hits(void);
 int64_t hj_count_i32(int32_t *r_alloc, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride,
                      int32_t *s_alloc, int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride);
 int32_t hj_probe_i32(int32_t *r_alloc, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride,

@@ -75,8 +75,12 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
 // slow: >= probe_tiles(src.n) words (tiles handed to the general path; the
 // count lives in meta[3])
 size_t probe_tiles(long long n);
+// slow_cap: entries of `slow` (tiles beyond it are never written; the
+// callers size it from probe_tiles / probe_tiles_xcd so that cannot happen)
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
-                        bool count_only, unsigned *slow, hipStream_t st);
+                        bool count_only, unsigned *slow, size_t slow_cap, hipStream_t st);
+// slow-list entries an XCD-grouped probe side of max_runs runs can need
+size_t probe_tiles_xcd(unsigned long long max_runs);
 
 // ---------------------------------------------------------------- radix join
 // (hj_radix.hip) partitions both relations by the top bits of the key hash
@@ -137,9 +141,15 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st);
 
+// Routing fan-out limit: k_part_scatter (> 512 parts) keeps 12 B of LDS
+// counters per part, k_part_hist 4 B (<= 96 KiB of the 160 KiB).
+constexpr int kMaxRouteParts = 8192;
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
                             hipStream_t st);
+
+// *neq |= 1 when the `bytes` (a multiple of 4) at a and b differ
+hipError_t launch_memeq(const void *a, const void *b, size_t bytes, unsigned long long *neq, hipStream_t st);
 
 // exclusive scan of a u64 array in place (hj_radix.hip); sums >= exclusive_scan_sums(len)
 hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,

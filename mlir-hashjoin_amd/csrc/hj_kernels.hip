@@ -240,7 +240,8 @@ __device__ __forceinline__ void probe_tiles(const SrcDev &src, unsigned &g, unsi
 // path, :539-549).  The cursor counts every match, so a caller whose
 // capacity was too small still learns the exact M (rows past cap dropped).
 template <int L, int FORM, bool WRITE>
-__global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out, unsigned *slow) {
+__global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out, unsigned *slow,
+                                                  unsigned long long slow_cap) {
     using LY = Lay<L>;
     using slot_t = typename LY::slot_t;
     using out_t = typename LY::out_t;
@@ -269,7 +270,10 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
         }
         if (!unique || __syncthreads_or(has_null ? 1 : 0)) {
             // general path: k_probe_slow takes this tile
-            if (threadIdx.x == 0) slow[atomicAdd(&t.meta[3], 1ull)] = (unsigned)(q * kXcdGroups + g);
+            if (threadIdx.x == 0) {
+                const unsigned long long j = atomicAdd(&t.meta[3], 1ull);
+                if (j < slow_cap) slow[j] = (unsigned)(q * kXcdGroups + g);   // (sized so it always is)
+            }
             continue;
         }
         slot_t S[kProbeItems];
@@ -352,7 +356,8 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
 // General path over the tiles k_probe handed over (slow[0 .. meta[3])):
 // persistent workgroups, one tile at a time.
 template <int L, int FORM, bool WRITE>
-__global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, OutDev out, const unsigned *slow) {
+__global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, OutDev out, const unsigned *slow,
+                                                       unsigned long long slow_cap) {
     using LY = Lay<L>;
     using slot_t = typename LY::slot_t;
     using out_t = typename LY::out_t;
@@ -366,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
 
     const slot_t *sl = (const slot_t *)t.slots;
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
-    const unsigned long long ntiles = t.meta[3];
+    const unsigned long long ntiles = t.meta[3] < slow_cap ? t.meta[3] : slow_cap;
     for (unsigned long long j = blockIdx.x; j < ntiles; j += gridDim.x) {
         if (threadIdx.x == 0) st_n = 0u;
         const unsigned id = slow[j];
@@ -918,17 +923,48 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
 }
 
 size_t probe_tiles(long long n) {
-    // plain tiles, or XCD-group tiles: a group's buckets are <= n / 512 full
-    // ones plus <= (256 workgroups + 2) x 8 open ones, 4 buckets per tile,
-    // one partial tile per group
-    return (size_t)(n > 0 ? (n + kProbeTile - 1) / kProbeTile : 0) + 1024;
+    // plain tiles: one slow-list entry per 2048-row tile at most
+    return (size_t)(n > 0 ? (n + kProbeTile - 1) / kProbeTile : 0) + 1;
+}
+
+size_t probe_tiles_xcd(unsigned long long max_runs) {
+    // XCD-group tiles: group g has ceil(runs_g / kXcdTileRuns) tiles, and the
+    // runs of all groups fit the set's run list (max_runs entries)
+    return (size_t)(max_runs / kXcdTileRuns) + kXcdGroups + 1;
+}
+
+// *neq |= 1 when two device byte ranges differ (host-memref count -> probe reuse)
+__global__ __launch_bounds__(256) void k_memeq(const unsigned *a, const unsigned *b, unsigned long long n,
+                                               unsigned long long *neq) {
+    bool diff = false;
+    const unsigned long long n4 = n / 4;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (unsigned long long)gridDim.x * 256) {
+        const uint4 x = ((const uint4 *)a)[i], y = ((const uint4 *)b)[i];
+        diff |= x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
+    }
+    for (unsigned long long i = n4 * 4 + (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (unsigned long long)gridDim.x * 256)
+        diff |= a[i] != b[i];
+    if (__syncthreads_or(diff ? 1 : 0) && threadIdx.x == 0) atomicOr(neq, 1ull);
+}
+
+hipError_t launch_memeq(const void *a, const void *b, size_t bytes, unsigned long long *neq, hipStream_t st) {
+    if (bytes % 4 != 0) return hipErrorInvalidValue;
+    const unsigned long long n = bytes / 4;
+    if (n == 0) return hipSuccess;
+    // uint4 loads need 16-B alignment of both (hipMalloc'd staging buffers are)
+    if ((((uintptr_t)a) | ((uintptr_t)b)) & 15) return hipErrorInvalidValue;
+    const unsigned long long blocks = (n / 4 + 255) / 256;
+    const unsigned g = (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
+    hipLaunchKernelGGL(k_memeq, dim3(g), dim3(256), 0, st, (const unsigned *)a, (const unsigned *)b, n, neq);
+    return hipGetLastError();
 }
 
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
-                        bool count_only, unsigned *slow, hipStream_t st) {
+                        bool count_only, unsigned *slow, size_t slow_cap, hipStream_t st) {
     if (src.n <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(&t.meta[3], 0, sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
+    const unsigned long long cap = slow_cap;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned tiles = grid_for(src.n, kProbeTile);
@@ -939,13 +975,13 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
 #define HJ_PROBE(L, F)                                                                                        \
     do {                                                                                                      \
         if (count_only) {                                                                                     \
-            hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow);      \
+            hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap); \
             hipLaunchKernelGGL((k_probe_slow<L, F, false>), dim3(gs), dim3(kBlock), 0, st, t, src, out,       \
-                               (const unsigned *)slow);                                                       \
+                               (const unsigned *)slow, cap);                                                  \
         } else {                                                                                              \
-            hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow);       \
+            hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap);  \
             hipLaunchKernelGGL((k_probe_slow<L, F, true>), dim3(gs), dim3(kBlock), 0, st, t, src, out,        \
-                               (const unsigned *)slow);                                                       \
+                               (const unsigned *)slow, cap);                                                  \
         }                                                                                                     \
     } while (0)
     if (layout == kWide) {

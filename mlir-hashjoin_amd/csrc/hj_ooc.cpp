@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "hj.h"
+#include "hj_internal.h"
 
 namespace {
 
@@ -273,7 +274,7 @@ extern "C" int64_t hj_host_join_ooc_i64(hj_ctx *c, const int64_t *rk, const int6
     }
     // grace: K groups of R that fit the budget (x1.5 headroom for skew)
     int K = 2;
-    while ((int64_t)K * r_fit < nr + nr / 2 && K < 65536) K *= 2;
+    while ((int64_t)K * r_fit < nr + nr / 2 && K < hj::kMaxRouteParts) K *= 2;   // (groups may then exceed the budget)
     std::lock_guard<std::mutex> lk(g_pool.mu);   // one grace join at a time uses the staging
     int64_t *hr = g_pool.get(0, (size_t)nr * 16), *hs = g_pool.get(1, (size_t)ns * 16);
     if (!hr || !hs) return HJ_ERR_NOMEM;

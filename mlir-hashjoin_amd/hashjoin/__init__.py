@@ -6,8 +6,8 @@ torch.distributed around it.  Importing fails loudly when libhj.so is
 missing: there is no CPU fallback.
 """
 from ._lib import HJError, check, declared_symbols, lib  # noqa: F401
-from .join import (HashJoin, gen_pkfk, gen_uniform_i32, gen_uniform_i64, gen_zipf,  # noqa: F401
+from .join import (HashJoin, device_info, gen_pkfk, gen_uniform_i32, gen_uniform_i64, gen_zipf,  # noqa: F401
                    hit_threshold, partition_of, zipf_params)
 
-__all__ = ["HashJoin", "HJError", "gen_pkfk", "gen_uniform_i32", "gen_uniform_i64", "hit_threshold",
+__all__ = ["HashJoin", "device_info", "HJError", "gen_pkfk", "gen_uniform_i32", "gen_uniform_i64", "hit_threshold",
            "partition_of", "gen_zipf", "zipf_params", "lib", "check", "declared_symbols"]

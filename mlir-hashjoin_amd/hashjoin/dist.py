@@ -1,9 +1,11 @@
 """Multi-GPU hash join: radix routing + RCCL all-to-all over xGMI.
 
 One process per GPU (torch.distributed, backend "nccl" == RCCL on ROCm).
-The reference is single-GPU (projectDescription.md:23-24 lists "Partitioned
-Hash-Join" as left out); north_star adds this path:
+The reference is single-GPU (projectDescription.md:23-25 lists "Partitioned
+Hash-Join" and "Joining skewed data" as left out); north_star adds this path
+(SURVEY 8(e)):
 
+  SHUFFLE (large build sides)
   1. every rank radix-partitions its slice of R and of S by the owner hash
      (hj_dev_partition_*: one HIP histogram + scatter pass each),
   2. per relation, one all-to-all of the per-owner counts (world int64),
@@ -11,10 +13,18 @@ Hash-Join" as left out); north_star adds this path:
      grouped send/recv) of packed 16-B {key, payload} tuples, started
      asynchronously: R's transfer overlaps S's routing, S's overlaps R's build,
   4. local build + probe on the received tuples (hj_dev_*_tuples_i64).
+     The output stays distributed: rank p holds the pairs whose key it owns.
 
-The output stays distributed: rank p holds the pairs whose key it owns.
-`exchange` is device-agnostic torch.distributed code, so the routing and
-exchange logic is exercised with gloo on CPU tensors in tests/.
+  REPLICATE (small build sides, |R| <= replicate_max_rows, SURVEY 8(e) "Small
+  R (C2-like)"): R's slices are all-gathered (one RCCL all-gather of at most
+  2^21 x 16 B = 32 MiB), every rank builds the whole R and probes its own S
+  slice in place -- S never crosses xGMI.  Rank p holds the pairs of its own
+  S rows.
+
+`exchange` / `distributed_join` are device-agnostic torch.distributed code:
+`hj` is anything with the HashJoin methods partition / build_tuples /
+probe_tuples, so the routing, exchange and replication logic runs with gloo
+on CPU tensors in tests/ (with the CPU oracle standing in for the kernels).
 """
 from __future__ import annotations
 
@@ -27,10 +37,15 @@ import torch.distributed as dist
 
 _DEBUG = os.environ.get("HJ_DEBUG") == "1"
 
+# Build sides up to this many rows (global) are replicated instead of routed
+# (32 MiB of tuples: one all-gather is cheaper than shuffling S).
+REPLICATE_MAX_ROWS = 1 << 21
+
 
 def _dbg(*a):
     if _DEBUG:
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         print(f"[hj.dist {time.time():.3f} rank {dist.get_rank()}]", *a, file=sys.stderr, flush=True)
 
 
@@ -42,18 +57,27 @@ def _dbg(*a):
 MAX_ROWS_PER_ROUND = 1 << 26
 
 
-def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows):
+def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows, self_p2p=False):
     """recv[rows from p] <- every p's send[rows for me]: one batched group of
     point-to-point messages of at most max_rows rows each (views, no staging
     copies).  Sender and receiver cut a slice into the same pieces because
-    in_rows on p and out_rows here describe the same slice.  Returns the
+    in_rows on p and out_rows here describe the same slice.  The slice a rank
+    keeps is copied locally unless self_p2p (tests: it then goes through the
+    backend like any other slice, cut into the same pieces).  Returns the
     outstanding works (wait on them before reading recv)."""
     world = len(in_rows)
     me = dist.get_rank(group)
     in_off = [sum(in_rows[:p]) for p in range(world)]
     out_off = [sum(out_rows[:p]) for p in range(world)]
-    recv[out_off[me]:out_off[me] + out_rows[me]].copy_(send[in_off[me]:in_off[me] + in_rows[me]])
     ops = []
+    if self_p2p:
+        gme = dist.get_global_rank(group, me) if group is not None else me
+        for a in range(0, in_rows[me], max_rows):
+            b = min(in_rows[me], a + max_rows)
+            ops.append(dist.P2POp(dist.isend, send[in_off[me] + a:in_off[me] + b], gme, group))
+            ops.append(dist.P2POp(dist.irecv, recv[out_off[me] + a:out_off[me] + b], gme, group))
+    else:
+        recv[out_off[me]:out_off[me] + out_rows[me]].copy_(send[in_off[me]:in_off[me] + in_rows[me]])
     for d in range(1, world):
         # pair ranks by distance so every link carries traffic at once
         to, fr = (me + d) % world, (me - d) % world
@@ -74,7 +98,7 @@ class Exchange:
     (batched point-to-point on the backend's stream).  `wait()` orders the
     current stream after the transfer; `recv` is valid from then on."""
 
-    def __init__(self, send, counts, group=None, max_rows=None):
+    def __init__(self, send, counts, group=None, max_rows=None, self_p2p=False):
         world = dist.get_world_size(group)
         if counts.numel() != world:
             raise ValueError("one count per rank required")
@@ -88,7 +112,7 @@ class Exchange:
         self.in_rows, self.out_rows = host[0].tolist(), host[1].tolist()
         self.send = send   # kept alive until the transfer is done
         self.recv = torch.empty((sum(self.out_rows), 2), dtype=torch.int64, device=send.device)
-        self._works = _all_to_all_rows(self.recv, send, self.out_rows, self.in_rows, group, max_rows)
+        self._works = _all_to_all_rows(self.recv, send, self.out_rows, self.in_rows, group, max_rows, self_p2p)
 
     def wait(self):
         for w in self._works:
@@ -110,23 +134,77 @@ def exchange(send_r, counts_r, send_s, counts_s, group=None, max_rows=None):
     return recv_r, recv_s, {"in_r": xr.in_rows, "in_s": xs.in_rows, "out_r": xr.out_rows, "out_s": xs.out_rows}
 
 
-def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None):
+def all_gather_rows(tuples, group=None):
+    """Every rank's (n_p, 2) int64 tuples, concatenated in rank order, on
+    every rank: counts all-gathered first, slices padded to the largest one
+    for one all_gather_into_tensor (RCCL all-gather), then compacted."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([tuples.shape[0]], dtype=torch.int64, device=tuples.device)
+    ns = torch.empty(world, dtype=torch.int64, device=tuples.device)
+    dist.all_gather_into_tensor(ns, n, group=group)
+    counts = ns.cpu().tolist()
+    mx = max(counts) if counts else 0
+    if mx == 0:
+        return torch.empty((0, 2), dtype=torch.int64, device=tuples.device)
+    pad = torch.zeros((mx, 2), dtype=torch.int64, device=tuples.device)
+    pad[:tuples.shape[0]].copy_(tuples)
+    full = torch.empty((world * mx, 2), dtype=torch.int64, device=tuples.device)
+    dist.all_gather_into_tensor(full, pad, group=group)
+    return torch.cat([full[p * mx:p * mx + counts[p]] for p in range(world)])
+
+
+def _probe_all(hj, tuples, capacity):
+    """Probe into an output sized optimistically, once more at the exact M."""
+    cap = max(1, tuples.shape[0] if capacity is None else int(capacity))
+    for _ in range(2):
+        out_r = torch.empty(cap, dtype=torch.int64, device=tuples.device)
+        out_s = torch.empty(cap, dtype=torch.int64, device=tuples.device)
+        cnt = hj.probe_tuples(tuples, out_r, out_s)
+        m = int(cnt.item())
+        if m <= cap:
+            return out_r[:m], out_s[:m]
+        cap = m
+    raise RuntimeError("distributed join output did not fit after resizing")
+
+
+def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None,
+                     replicate_max_rows=None, max_rows=None, self_p2p=False):
     """Join this rank's slices of R and S against every other rank's.
 
-    hj: a hashjoin.HashJoin on this rank's GPU.  Returns this rank's share of
-    the result (out_r, out_s) = (R.pay, S.pay) of every pair whose key this
-    rank owns.  Transfers overlap compute: R's tuples move while S is routed,
-    S's while R is built.  `phases`, if a dict, receives CUDA events
-    (start, routed, built, probed) for timing and "rows" = (received R rows,
-    received S rows)."""
-    world = dist.get_world_size(group)
-    ev = (lambda name: _event(phases, name)) if phases is not None else (lambda name: None)
+    hj: a hashjoin.HashJoin on this rank's GPU (or any object with its
+    partition / build_tuples / probe_tuples methods).  Returns this rank's
+    share of the result (out_r, out_s) = (R.pay, S.pay): the pairs of keys it
+    owns (shuffle) or of its own S rows (replicate).  `phases`, if a dict,
+    receives events (start, routed, built, probed) for timing (CUDA events on
+    GPU tensors, else host timestamps), "rows" = (R rows built, S rows
+    probed) and "mode" = "shuffle" | "replicate"."""
+    if replicate_max_rows is None:
+        replicate_max_rows = REPLICATE_MAX_ROWS
+    cuda = rkey.is_cuda
+    ev = (lambda name: _event(phases, name, cuda)) if phases is not None else (lambda name: None)
     ev("start")
+    n_r = torch.tensor([rkey.numel()], dtype=torch.int64, device=rkey.device)
+    dist.all_reduce(n_r, group=group)
+    if int(n_r.item()) <= replicate_max_rows:
+        # small build side: every rank builds all of R, S stays where it is
+        _dbg("replicate", int(n_r.item()), skey.numel())
+        mine = torch.stack([rkey, rpay], dim=1).contiguous()
+        all_r = all_gather_rows(mine, group)
+        local_s = torch.stack([skey, spay], dim=1).contiguous()
+        ev("routed")
+        hj.build_tuples(all_r)
+        ev("built")
+        if phases is not None:
+            phases["rows"] = (all_r.shape[0], local_s.shape[0])
+            phases["mode"] = "replicate"
+        out = _probe_all(hj, local_s, capacity)
+        ev("probed")
+        return out
     _dbg("route", rkey.numel(), skey.numel())
-    send_r, cr = hj.partition(rkey, rpay, world)
-    xr = Exchange(send_r, cr, group)
-    send_s, cs = hj.partition(skey, spay, world)
-    xs = Exchange(send_s, cs, group)
+    send_r, cr = hj.partition(rkey, rpay, dist.get_world_size(group))
+    xr = Exchange(send_r, cr, group, max_rows, self_p2p)
+    send_s, cs = hj.partition(skey, spay, dist.get_world_size(group))
+    xs = Exchange(send_s, cs, group, max_rows, self_p2p)
     ev("routed")
     recv_r = xr.wait()
     _dbg("build", recv_r.shape[0])
@@ -136,21 +214,30 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     _dbg("probe", recv_s.shape[0])
     if phases is not None:
         phases["rows"] = (recv_r.shape[0], recv_s.shape[0])
-    cap = max(1, recv_s.shape[0] if capacity is None else int(capacity))
-    for _ in range(2):
-        out_r = torch.empty(cap, dtype=torch.int64, device=recv_s.device)
-        out_s = torch.empty(cap, dtype=torch.int64, device=recv_s.device)
-        cnt = hj.probe_tuples(recv_s, out_r, out_s)
-        ev("probed")
-        m = int(cnt.item())
-        if m <= cap:
-            return out_r[:m], out_s[:m]
-        cap = m
-    raise RuntimeError("distributed join output did not fit after resizing")
+        phases["mode"] = "shuffle"
+    out = _probe_all(hj, recv_s, capacity)
+    ev("probed")
+    return out
 
 
-def _event(store, name):
-    e = torch.cuda.Event(enable_timing=True)
-    e.record()
+class _HostMark:
+    """Host-clock stand-in for a CUDA event (CPU tensors)."""
+
+    def __init__(self):
+        self.t = time.perf_counter()
+
+    def synchronize(self):
+        pass
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1000.0
+
+
+def _event(store, name, cuda=True):
+    if not cuda:
+        e = _HostMark()
+    else:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
     store[name] = e
     return e

@@ -339,6 +339,15 @@ def gen_uniform_i32(seed, stream_id, lo, hi, n, i0=0, device=None, stream=None):
     return k
 
 
+def device_info(device=0):
+    """hipDeviceProp facts the roofline quotes (hj_device_info)."""
+    a = (C.c_int64 * 8)()
+    check(lib.hj_device_info(int(device), a), "hj_device_info")
+    keys = ("cus", "memory_clock_khz", "memory_bus_bits", "l2_bytes", "hbm_bytes", "shader_clock_khz",
+            "lds_bytes_per_cu", "peak_mb_per_s")
+    return dict(zip(keys, [int(x) for x in a]))
+
+
 def partition_of(key: int, nparts: int) -> int:
     """Owner of a key under the routing hash (host function of libhj.so)."""
     return int(lib.hj_partition_of(int(key), int(nparts)))

@@ -59,7 +59,11 @@ def main():
         allj = json.load(open(path))
     except (OSError, ValueError):
         allj = {}
-    allj[f"{config}/n{n}"] = {"source": note, "kernels": kernels}
+    # the kernel sources these counters belong to: bench.py reports the
+    # traffic only while they are unchanged
+    sys.path.insert(0, os.path.dirname(HERE))
+    from bench import kernel_source_sha
+    allj[f"{config}/n{n}"] = {"source": note, "source_sha": kernel_source_sha(), "kernels": kernels}
     json.dump(allj, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps(allj[f"{config}/n{n}"], indent=1))
 

@@ -95,3 +95,102 @@ def test_two_rank_exchange_join(case, tmp_path, oracle):
         sk, sp = oracle.gen_uniform_i64(case["seed"], 2, 1, case["hi"], case["NS"])
         er, es = oracle.nested_loop_i64(rk, rp, sk, sp)
     assert oracle.same_multiset(np.concatenate(rs), np.concatenate(ss), er, es)
+
+
+# ---------------------------------------------------------------------------
+# distributed_join itself (routing / replication, capacity retry, pieces) with
+# the device kernels replaced by CPU stand-ins: partition = the numpy
+# restatement of the routing hash, build/probe = the oracle's join_v2
+# restatement.  The composition is the product's hashjoin.dist code.
+class _CpuJoin:
+    """HashJoin's partition / build_tuples / probe_tuples on CPU tensors."""
+
+    def __init__(self):
+        from oracle import pyoracle as O
+        self.O = O
+        self.r = None
+        self.calls = {"partition": 0, "build": 0, "probe": 0}
+
+    def partition(self, key, pay, nparts):
+        self.calls["partition"] += 1
+        return _route(key.numpy(), pay.numpy(), nparts)
+
+    def build_tuples(self, t):
+        self.calls["build"] += 1
+        self.r = t.numpy().copy()
+
+    def probe_tuples(self, t, out_r, out_s):
+        self.calls["probe"] += 1
+        s = t.numpy()
+        o_r, o_s = self.O.chained_join_i64(self.r[:, 0], self.r[:, 1], s[:, 0], s[:, 1], H=max(1, len(self.r)))
+        m = len(o_r)
+        k = min(m, out_r.numel())
+        out_r[:k] = torch.from_numpy(o_r[:k])
+        out_s[:k] = torch.from_numpy(o_s[:k])
+        return torch.tensor([m], dtype=torch.int64)
+
+
+def _relations(case, rank, world):
+    from oracle import pyoracle as O
+    NR, NS = case["NR"], case["NS"]
+    r0, nr = rank * NR // world, (rank + 1) * NR // world - rank * NR // world
+    s0, ns = rank * NS // world, (rank + 1) * NS // world - rank * NS // world
+    if case["dist"] == "pkfk":
+        return O.gen_pkfk_i64(case["seed"], NR, NS, case["frac"], r0, nr, s0, ns)
+    rk, rp = O.gen_uniform_i64(case["seed"], 1, case.get("lo", 1), case["hi"], nr, i0=r0)
+    sk, sp = O.gen_uniform_i64(case["seed"], 2, case.get("lo", 1), case["hi"], ns, i0=s0)
+    return rk, rp, sk, sp
+
+
+def _dj_worker(rank, world, port, case, outdir):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mlir-hashjoin_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hashjoin.dist import distributed_join
+    from test_abi import _np_partition_of
+    rk, rp, sk, sp = (torch.from_numpy(x) for x in _relations(case, rank, world))
+    hj = _CpuJoin()
+    ph = {}
+    o_r, o_s = distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
+                                replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"))
+    nrows = ph["rows"]
+    if ph["mode"] == "shuffle":
+        # every output key is owned here (S.pay of the generators is the global row id)
+        assert hj.calls["partition"] == 2
+        full_sk = _relations(case, 0, 1)[2]
+        if o_s.numel():
+            assert (_np_partition_of(full_sk[o_s.numpy()], world) == rank).all()
+    else:
+        assert hj.calls["partition"] == 0 and nrows[0] == case["NR"]
+    assert ph["start"].elapsed_time(ph["probed"]) >= 0.0
+    np.savez(os.path.join(outdir, f"dj{rank}.npz"), r=o_r.numpy(), s=o_s.numpy(), nr=np.array([nrows[0]]),
+             ns=np.array([nrows[1]]), mode=np.array([ph["mode"] == "shuffle"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=21),
+    dict(dist="uniform", NR=2000, NS=2500, hi=300, seed=22),                    # duplicates both sides
+    dict(dist="uniform", NR=1500, NS=1800, lo=-(1 << 63), hi=-(1 << 63) + 40, seed=23),  # INT64_MIN keys
+    dict(dist="pkfk", NR=4000, NS=6001, frac=0.9, seed=24, capacity=1, world=3),  # output resized
+    dict(dist="pkfk", NR=3001, NS=4999, frac=0.7, seed=25, max_rows=97),       # slices cut in pieces
+    dict(dist="pkfk", NR=700, NS=9000, frac=1.0, seed=26, replicate=1 << 21),  # small R: replicated
+    dict(dist="uniform", NR=900, NS=1200, hi=50, seed=27, replicate=1 << 21, world=3, capacity=5),
+    dict(dist="pkfk", NR=5, NS=3, frac=1.0, seed=28, world=4),                 # ranks without rows
+], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
+        "tiny_4ranks"])
+def test_distributed_join_gloo(case, tmp_path, oracle):
+    world = case.get("world", 2)
+    mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
+    rs, ss = [], []
+    for k in range(world):
+        with np.load(tmp_path / f"dj{k}.npz", allow_pickle=False) as z:
+            rs.append(z["r"]); ss.append(z["s"])
+    parts = [_relations(case, k, world) for k in range(world)]
+    rk, rp, sk, sp = (np.concatenate([p[i] for p in parts]) for i in range(4))
+    er, es = oracle.nested_loop_i64(rk, rp, sk, sp)
+    assert oracle.same_multiset(np.concatenate(rs), np.concatenate(ss), er, es)

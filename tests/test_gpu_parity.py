@@ -105,6 +105,59 @@ def test_memref_offsets_and_strides(oracle):
     assert MR.probe_i32(r, s, np.empty(m + 1, np.int32), np.empty(m + 1, np.int32)) == hashjoin._lib.HJ_ERR_CAPACITY
 
 
+def test_memref_count_then_probe_reuses_the_join(oracle):
+    """@countRows -> @probeRelation on the same inputs: the probe call returns
+    the count call's pairs (no second build / probe); changed inputs at the
+    same address get a fresh join (join_v1.mlir:110-176)."""
+    r = oracle.gen_uniform_i32(9, 1, 1, 300, 20000)
+    s = oracle.gen_uniform_i32(9, 2, 1, 300, 15000)
+    h0 = hashjoin.lib.hj_host_memo_hits()
+    m = MR.count_i32(r, s)
+    o_r = np.empty(m, np.int32); o_s = np.empty(m, np.int32)
+    assert MR.probe_i32(r, s, o_r, o_s) == 0
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 1
+    assert oracle.same_multiset(o_r, o_s, *oracle.nested_loop_i32(r, s))
+    s[:100] = 7                                  # same buffer, new contents
+    m2 = MR.count_i32(r, s)
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 1
+    exp2 = oracle.nested_loop_i32(r, s)
+    assert m2 == len(exp2[0])
+    o_r = np.empty(m2, np.int32); o_s = np.empty(m2, np.int32)
+    assert MR.probe_i32(r, s, o_r, o_s) == 0
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 2
+    assert oracle.same_multiset(o_r, o_s, *exp2)
+    # i64 columns: reused too, and an i32 join in between invalidates nothing wrongly
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(12, 5000, 7000, 0.6)
+    m3 = MR.count_i64(rk, rp, sk, sp)
+    o_r = np.empty(m3, np.int64); o_s = np.empty(m3, np.int64)
+    assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 3
+    assert oracle.same_multiset(o_r, o_s, *oracle.nested_loop_i64(rk, rp, sk, sp))
+
+
+def test_memref_concurrent_host_threads(oracle):
+    """Host entry points share one default context: concurrent callers are
+    serialised by its lock, each gets its own join."""
+    import threading
+    cases = [(oracle.gen_uniform_i32(20 + i, 1, 1, 200 + 50 * i, 6000 + 500 * i),
+              oracle.gen_uniform_i32(20 + i, 2, 1, 200 + 50 * i, 5000 + 300 * i)) for i in range(6)]
+    res = [None] * len(cases)
+
+    def run(i):
+        r, s = cases[i]
+        for _ in range(3):
+            out = MR.ciface_join_i32(r, s)
+            res[i] = out
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(cases))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for (r, s), out in zip(cases, res):
+        assert oracle.same_multiset(out[:, 0], out[:, 1], *oracle.nested_loop_i32(r, s))
+
+
 # ------------------------------------------------------------------ random vs oracle
 CASES = [
     ("uniform_i64", 64, 5000, 7000, 1, 300),
@@ -224,7 +277,13 @@ def test_datagen_matches_oracle(oracle):
     assert np.array_equal(host(k32), oracle.gen_uniform_i32(3, 9, -(1 << 31), (1 << 31) - 1, 4000))
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 8, 257])
+def test_partition_fanout_limit(hj):
+    k = torch.arange(100, dtype=torch.int64, device="cuda")
+    with pytest.raises(hashjoin.HJError):
+        hj.partition(k, k, 8193)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 8, 257, 1000, 4096, 8192])
 def test_partition_kernel(hj, oracle, P):
     from test_abi import _np_partition_of
     k, p = oracle.gen_uniform_i64(P, 1, -(1 << 62), 1 << 62, 12345)
