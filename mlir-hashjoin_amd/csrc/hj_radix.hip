@@ -855,15 +855,20 @@ __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, c
 // ABL (diagnostics only, micro/join_micro.hip; the product uses 0) switches
 // phases off: 1 no cursor atomic, 2 no output writes, 4 no probe, 8 no build,
 // 16 probe reads the first slot only.
-template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems>
-__global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per SIMD: <= 128 VGPRs
+// WPS: minimum waves per SIMD (4: <= 128 VGPRs, 2 workgroups of 512 per CU;
+// 2: <= 256 VGPRs).  RCAPX: build rows per round (0: 5/8 of the slots).
+// PF: prefetch the next item's first R round and S sub-chunk into registers
+// while this item is probed (needs the register room of WPS = 2).
+template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems, int WPS = 4, int RCAPX = 0,
+          bool PF = false>
+__global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // output element
     constexpr int TS = 1 << TSL;
     constexpr unsigned kMask = TS - 1;
     constexpr int SI = SI_;                   // S rows per thread per sub-chunk
-    constexpr int RCAP = TS * 5 / 8;          // build rows per round (load factor <= 0.625)
+    constexpr int RCAP = RCAPX ? RCAPX : TS * 5 / 8;   // build rows per round (load factor <= 0.625)
     constexpr int RI = RCAP / NT;             // build rows per thread per round
     constexpr int SUBR = NT * SI;             // rows per sub-chunk
     constexpr unsigned rb = (unsigned)RCAP >> kRunLog;       // runs per build round
@@ -933,14 +938,24 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
         ents(a.s_runs, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
         return rows_of(srows, es, sv_, SI);
     };
+    T nsv_[PF ? SI : 1];
+    unsigned nsok = 0;
+    bool have_next = false;   // PF: this item's first R round / S sub-chunk already in registers
     while (true) {
         // this item's first R round and first S sub-chunk: issued before the
         // table init so their latency hides behind it.  (Prefetching the next
-        // item's R rows instead costs VGPRs -> spills, and measured slower:
-        // profiles/r01_micro_join_buckets.txt; its list entries and the
-        // descriptor after it are prefetched instead.)
-        rok = rows_of(rrows, er, rv_, RI);
-        sok = rows_of(srows, es, sv_, SI);
+        // item's R rows instead costs VGPRs -> spills at 4 waves per SIMD, and
+        // measured slower: profiles/r01_micro_join_buckets.txt; PF does it at
+        // 2 waves per SIMD.)
+        if (!have_next) {
+            rok = rows_of(rrows, er, rv_, RI);
+            sok = rows_of(srows, es, sv_, SI);
+        } else if constexpr (PF) {
+#pragma unroll
+            for (int i = 0; i < SI; ++i) sv_[i] = nsv_[i];
+            sok = nsok;
+        }
+        have_next = false;
         const bool more = w + gridDim.x < total;
         u64 ner[RI], nes[SI];
         ItemDesc nnx = nx;
@@ -994,6 +1009,14 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             if (dup) s_dup = 1u;
             __syncthreads();
             const bool unique = s_dup == 0u;
+            if constexpr (PF) {
+                // the build's rows are dead: the next item's first R round
+                // flies while this item is probed
+                if (more && r0 + rb >= it.r_hi) {
+                    rok = rows_of(rrows, ner, rv_, RI);
+                    have_next = true;
+                }
+            }
             // once per workgroup: every table with a repeated key storing to
             // the one flag serialised those stores at the memory side (C1-ref
             // at 2^28: +3.5 ms, micro/join_micro.hip mode 1)
@@ -1005,13 +1028,18 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
             // ---- probe the chunk, one sub-chunk of S rows at a time
             for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
                 if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
+                if constexpr (PF) {
+                    // last sub-chunk of the last round: the next item's first
+                    // S sub-chunk flies while this one is probed and written
+                    if (have_next && sb + subb >= it.s_hi) nsok = rows_of(srows, nes, nsv_, SI);
+                }
                 // first slot of every row read before any is resolved (SI
                 // independent LDS reads in flight); most rows end there
                 unsigned m[SI], hp[SI];
                 u64 e0[SI];
                 bool pa[SI];
                 u64 cnt = 0;
-                unsigned mb = 0u;   // general path: bit i = row slot i has a match
+                unsigned mb = 0u;   // general path, wide rows: bit i = row slot i has a match
 #pragma unroll
                 for (int i = 0; i < SI; ++i) {
                     m[i] = 0xFFFFFFFFu;
@@ -1069,7 +1097,14 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                 } else {
                     // every chain walks to EMPTY (a key may repeat); row
                     // slots in pairs as above
+                    // (narrow rows: m[i] counts row slot i's matches on this
+                    // path, for the cooperative writes below; wide rows keep
+                    // one bit each in mb -- five live counts spilled there)
                     auto hit = [&](u64 e, u64 key) { return (WIDE ? e : (e >> 32)) == key; };
+                    if constexpr (!WIDE) {
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) m[i] = 0u;
+                    }
 #pragma unroll
                     for (int i = 0; i < SI; i += 2) {
                         const int j = i + 1 < SI ? i + 1 : i;
@@ -1082,7 +1117,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                             if (la) {
                                 if (hit(ea, ka)) {
                                     ++cnt;
-                                    mb |= 1u << i;
+                                    if constexpr (WIDE) mb |= 1u << i;
+                                    else ++m[i];
                                 }
                                 ha = (ha + 1) & kMask;
                                 ea = tkey[ha];
@@ -1090,7 +1126,8 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                             if (lb) {
                                 if (hit(eb, kb)) {
                                     ++cnt;
-                                    mb |= 1u << j;
+                                    if constexpr (WIDE) mb |= 1u << j;
+                                    else ++m[j];
                                 }
                                 hb = (hb + 1) & kMask;
                                 eb = tkey[hb];
@@ -1162,6 +1199,56 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                     if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, tot);
                     __syncthreads();
                     u64 pos = s_base + pre;
+                    // (narrow rows only: in the wide kernel the extra state cost
+                    // the duplicate-free path a scratch spill)
+                    if (!WIDE && !unique && tot > (u64)(2 * SUBR)) {
+                        // many matches per probe row (the reference's 10M x 10M
+                        // keys in [1, 100k] workload: ~100 each): a lane's own
+                        // pairs would go out as one partial line per lane and
+                        // store.  Instead the wave takes its rows one at a time
+                        // and scans the row's chain 64 slots per step, one slot
+                        // per lane; matching lanes write consecutive positions.
+                        const unsigned lane = threadIdx.x & 63u;
+                        const u64 lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            if constexpr ((ABL & 2) != 0) break;
+                            const u64 key_i = R::key(sv_[i]);
+                            const u64 pay_i = (u64)R::pay(sv_[i]);
+                            const u64 pos_i = pos;
+                            pos += m[i];
+                            for (int l = 0; l < 64; ++l) {
+                                if (__builtin_amdgcn_readlane((int)m[i], l) == 0) continue;   // uniform
+                                const u64 k = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(key_i >> 32), l) << 32) |
+                                              (u64)(unsigned)__builtin_amdgcn_readlane((int)key_i, l);
+                                const PT sp_ = (PT)(((u64)(unsigned)__builtin_amdgcn_readlane((int)(pay_i >> 32), l) << 32) |
+                                                    (u64)(unsigned)__builtin_amdgcn_readlane((int)pay_i, l));
+                                u64 p = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(pos_i >> 32), l) << 32) |
+                                        (u64)(unsigned)__builtin_amdgcn_readlane((int)pos_i, l);
+                                unsigned h = (unsigned)(rhash(k) >> a.tshift) & kMask;
+                                while (true) {
+                                    const unsigned hs = (h + lane) & kMask;
+                                    const u64 e = tkey[hs];
+                                    const u64 emp = __ballot(e == kEmpty);
+                                    const unsigned lim = emp ? (unsigned)__ffsll((long long)emp) - 1u : 64u;
+                                    const bool hitm = lane < lim && (WIDE ? e : (e >> 32)) == k;
+                                    const u64 mm = __ballot(hitm);
+                                    if (hitm) {
+                                        const u64 q = p + (u64)__popcll(mm & lt);
+                                        if (q < (u64)a.cap) {
+                                            orr[q] = WIDE ? (PT)tpay[hs] : (PT)(e & 0xffffffffull);
+                                            oss[q] = sp_;
+                                        }
+                                    }
+                                    p += (u64)__popcll(mm);
+                                    if (emp) break;
+                                    h = (h + 64u) & kMask;
+                                }
+                            }
+                        }
+                        __syncthreads();   // s_base reused by the next sub-chunk
+                        continue;
+                    }
 #pragma unroll
                     for (int i = 0; i < SI; ++i) {
                         if constexpr ((ABL & 2) != 0) break;
@@ -1178,7 +1265,7 @@ __global__ __launch_bounds__(NT, 4) void k_join(JoinArgs a) {   // 4 waves per S
                             const u64 key = R::key(sv_[i]);
                             // rows without a match skip the second walk (with
                             // duplicate keys most probes still miss: C1-ref)
-                            if (!((mb >> i) & 1u)) continue;
+                            if (WIDE ? !((mb >> i) & 1u) : !m[i]) continue;
                             unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
                             while (true) {
                                 const u64 e = tkey[h];

@@ -149,19 +149,16 @@ int main(int argc, char **argv) {
         a.tshift = 64 - pl.total_bits - TSL;                                                              \
         hipLaunchKernelGGL((k_join<true, WR, TSL, NT, ABL>), dim3(PER_CU * cus), dim3(NT), 0, 0, a);      \
     })
-#define J2(WR, ABL, SI, NAME)                                                                               \
+#define JP(TSL, NT, PER_CU, SI, WPS, RCAP, PF, NAME)                                                      \
     run(NAME, [&] {                                                                                       \
-        a.tshift = 64 - pl.total_bits - kJ2NBL;                                                           \
-        hipLaunchKernelGGL((k_join2<true, WR, kJ2NT, kJ2RI, kJ2NBL, SI, ABL>), dim3(2 * cus), dim3(kJ2NT), 0, 0, a); \
+        a.tshift = 64 - pl.total_bits - TSL;                                                              \
+        hipLaunchKernelGGL((k_join<true, true, TSL, NT, 0, SI, WPS, RCAP, PF>), dim3(PER_CU * cus), dim3(NT), 0, 0, a); \
     })
-    J2(true, 0, 5, "k_join2 SI5 full");
-    J2(false, 0, 5, "k_join2 SI5 count only");
-    J2(true, 3, 5, "k_join2 SI5 no atomic, no writes");
-    J2(true, 0, 3, "k_join2 SI3 full");
-    J2(false, 0, 3, "k_join2 SI3 count only");
-    J2(true, 0, 2, "k_join2 SI2 full");
-    J2(false, 0, 2, "k_join2 SI2 count only");
-    J2(true, 3, 2, "k_join2 SI2 no atomic, no writes");
+    JP(13, 512, 1, 5, 2, 2560, true, "PF 8192 slots, 512 thr, 1/CU");
+    JP(13, 512, 1, 5, 2, 2560, false, "noPF 8192 slots, 512 thr, 1/CU");
+    JP(12, 512, 1, 5, 2, 2560, true, "PF 4096 slots, 512 thr, 1/CU");
+    JP(13, 1024, 1, 3, 4, 3072, true, "PF 8192 slots, 1024 thr, 1/CU");
+    JP(13, 1024, 1, 3, 4, 3072, false, "noPF 8192 slots, 1024 thr, 1/CU");
     J(12, 512, 2, true, 0, "full");
     J(12, 512, 2, false, 0, "count only");
     J(12, 512, 2, true, 1, "no atomic");

@@ -236,3 +236,17 @@ def test_radix_hot_key_tiles(hj, oracle, bits):
     sp = np.arange(n, dtype=np.int64)
     o = run(hj, rk, rp, sk, sp, bits)
     assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=4096))
+
+
+@pytest.mark.parametrize("bits", [3, 7])
+def test_radix_i32_many_matches_per_row(hj, oracle, bits):
+    """~100 build copies per key (the reference's 10M x 10M / [1, 100k] shape,
+    scaled down): sub-chunks with > 2 matches per probe row take the wave-
+    cooperative write path; pairs must equal the oracle's."""
+    r = oracle.gen_uniform_i32(70 + bits, 1, 1, 400, 40000)
+    s = oracle.gen_uniform_i32(70 + bits, 2, 1, 400, 30000)
+    s[:7] = 999                     # no match
+    o = run(hj, r, None, s, None, bits)
+    exp = oracle.chained_join_i32(r, s, H=400)
+    assert len(o[0]) == len(exp[0]) > 2 * len(s)
+    assert oracle.same_multiset(*o, exp[0].astype(np.int64), exp[1].astype(np.int64))
