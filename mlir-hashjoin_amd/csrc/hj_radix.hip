@@ -1026,12 +1026,30 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
             }
 
             // ---- probe the chunk, one sub-chunk of S rows at a time
+            bool have_sub = false;   // PF: this sub-chunk's rows are already in nsv_
             for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
-                if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
+                if (sb != it.s_lo || r0 != it.r_lo) {
+                    if (PF && have_sub) {
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) sv_[i] = nsv_[i];
+                        sok = nsok;
+                    } else {
+                        sok = load_s(sb);
+                    }
+                }
+                have_sub = false;
                 if constexpr (PF) {
-                    // last sub-chunk of the last round: the next item's first
-                    // S sub-chunk flies while this one is probed and written
-                    if (have_next && sb + subb >= it.s_hi) nsok = rows_of(srows, nes, nsv_, SI);
+                    // the next sub-chunk of this round (many-sub-chunk items:
+                    // C2) or, after the last one, the next item's first
+                    // sub-chunk flies while this one is probed and written
+                    if (sb + subb < it.s_hi) {
+                        u64 e2[SI];
+                        ents(a.s_runs, sb + subb, sb + 2 * subb < it.s_hi ? sb + 2 * subb : it.s_hi, e2, SI);
+                        nsok = rows_of(srows, e2, nsv_, SI);
+                        have_sub = true;
+                    } else if (have_next) {
+                        nsok = rows_of(srows, nes, nsv_, SI);
+                    }
                 }
                 // first slot of every row read before any is resolved (SI
                 // independent LDS reads in flight); most rows end there
@@ -1700,9 +1718,12 @@ JoinVariant join_variant() {
     }();
     static int kind = [] {
         const char *e = getenv("HJ_JOIN");
-        return (e && atoi(e) == 2) ? 2 : 1;
+        const int v = e ? atoi(e) : 1;
+        return (v >= 1 && v <= 4) ? v : 1;
     }();
     if (kind == 2) return JoinVariant{12, 512, 2, kJ2SI};
+    if (kind == 3) return JoinVariant{13, 512, 3, 5};   // prefetching k_join, 1 workgroup per CU, 8192 slots
+    if (kind == 4) return JoinVariant{12, 512, 4, 3};   // prefetching k_join, 2 workgroups per CU, 3 S rows
     return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256), 1, kJoinItems};
 }
 
@@ -1920,7 +1941,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     const JoinVariant jv = join_variant();
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
     // persistent grid: as many workgroups as fit at once (LDS-limited)
-    const int per_cu = jv.kind == 2 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
+    const int per_cu = jv.kind == 2 || jv.kind == 4 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
     const unsigned pg = (unsigned)(per_cu * cu_count());
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
@@ -1961,7 +1982,27 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     } while (0)
 #define HJ_JOIN2(W, WR) \
     hipLaunchKernelGGL((k_join2<W, WR, kJ2NT, kJ2RI, kJ2NBL, kJ2SI>), dim3(grid), dim3(kJ2NT), 0, st, a)
-    if (jv.kind == 2) {
+#define HJ_JOINP(W, WR, TSL, SI, WPS)                                                                        \
+    hipLaunchKernelGGL((k_join<W, WR, TSL, 512, 0, SI, WPS, 2560, true>), dim3(grid), dim3(512), 0, st, a)
+    if (jv.kind == 3 || jv.kind == 4) {
+        if (jv.kind == 3) {
+            if (wide) {
+                if (count_only) HJ_JOINP(true, false, 13, 5, 2);
+                else HJ_JOINP(true, true, 13, 5, 2);
+            } else {
+                if (count_only) HJ_JOINP(false, false, 13, 5, 2);
+                else HJ_JOINP(false, true, 13, 5, 2);
+            }
+        } else {
+            if (wide) {
+                if (count_only) HJ_JOINP(true, false, 12, 3, 4);
+                else HJ_JOINP(true, true, 12, 3, 4);
+            } else {
+                if (count_only) HJ_JOINP(false, false, 12, 3, 4);
+                else HJ_JOINP(false, true, 12, 3, 4);
+            }
+        }
+    } else if (jv.kind == 2) {
         if (wide) {
             if (count_only) HJ_JOIN2(true, false);
             else HJ_JOIN2(true, true);
@@ -1976,6 +2017,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         if (count_only) HJ_JOIN_V(false, false);
         else HJ_JOIN_V(false, true);
     }
+#undef HJ_JOINP
 #undef HJ_JOIN2
 #undef HJ_JOIN_V
 #undef HJ_JOIN
