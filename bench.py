@@ -437,8 +437,8 @@ def main():
         },
         "device": {"name": torch.cuda.get_device_name(local), **info,
                    "peak_used_gbs": HBM_PEAK_GBS,
-                   "peak_note": "8.0 TB/s spec (MI355X_MICROARCH.md); 2 x memory clock x bus width of "
-                                "hipDeviceProp is peak_mb_per_s"},
+                   "peak_note": "8.0 TB/s spec (MI355X_MICROARCH.md); peak_mb_per_s = hipDeviceProp "
+                                "memoryBusWidth/8 x memoryClockRate x 4 (HBM3E transfers per reported clock)"},
     }
     if a.config in REFERENCE_PUBLISHED:
         pub = REFERENCE_PUBLISHED[a.config]

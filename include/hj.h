@@ -61,7 +61,8 @@ int hj_abi_version(void);
 const char *hj_last_error(void);
 /* Device facts for the roofline: [0] CUs, [1] memory clock (kHz), [2] memory
  * bus width (bits), [3] L2 bytes (one XCD), [4] HBM bytes, [5] shader clock
- * (kHz), [6] LDS bytes per CU, [7] 2 x memory clock x bus width (MB/s). */
+ * (kHz), [6] LDS bytes per CU, [7] peak HBM MB/s = 4 x memory clock x bus
+ * bytes (HBM3E: 4 transfers per reported clock). */
 int hj_device_info(int device, int64_t out[8]);
 
 /* ------------------------------------------------------------------ context

@@ -868,8 +868,9 @@ int hj_device_info(int device, int64_t out[8]) {
     out[4] = (int64_t)p.totalGlobalMem;
     out[5] = p.clockRate;         // kHz
     out[6] = (int64_t)p.maxSharedMemoryPerMultiProcessor;
-    // DDR: two transfers per memory clock
-    out[7] = (int64_t)(2.0 * (double)p.memoryClockRate * 1e3 * (double)p.memoryBusWidth / 8.0 / 1e6);   // MB/s
+    // HBM3E: 4 transfers per reported memory clock (MI355X reports 2.0 GHz
+    // and 8192 bits: 8 Gb/s per pin, 8.19 TB/s -- the 8.0 TB/s spec)
+    out[7] = (int64_t)(4.0 * (double)p.memoryClockRate * 1e3 * (double)p.memoryBusWidth / 8.0 / 1e6);   // MB/s
     return HJ_OK;
 }
 
