@@ -15,7 +15,7 @@ join of the whole relations with inputs resident in HBM:
 value = |S| / (time per step), the whole job over all ranks (max over ranks).
 `roofline` is SURVEY 8(d)'s probe-phase figure: 48 B per probe tuple (16 B S
 row + 16 B slot + 16 B output pair) over the probe phase's HIP-event time;
-`roofline.kernel` is the same for the dominant kernel (k_join) alone.
+`roofline.kernel` is the same for the dominant kernel (k_join_u) alone.
 Launch:  python bench.py [--gpus 1 --steps K --warmup W --config C3]
          python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
@@ -56,7 +56,10 @@ REFERENCE_PUBLISHED = {
     "REF-A": {"join_v1_s": 2.0, "join_v2_s": 1.5, "source": "join-performances.md:3-6, :16-19"},
     "REF-B": {"join_v1_s": 12.0, "join_v2_s": 12.5, "source": "join-performances.md:8-11, :21-24"},
 }
-PROBE_KERNELS = ("k_pass", "k_join")   # probe phase: S partition passes + the LDS join
+# probe phase: S partition passes + the LDS join (k_join_u; k_join takes the
+# items k_join_u defers -- none at C1-C4 -- and is counted when it ran)
+PROBE_KERNELS = ("k_pass", "k_join_u")
+OPTIONAL_PROBE_KERNELS = ("k_join",)
 
 
 def parse():
@@ -189,13 +192,14 @@ def pmc_record(config, n_gpus):
     return e, f"rocprofv3 PMC, {e.get('source', '')}"
 
 
-def traffic_of(rec, names):
-    """HBM bytes per launch summed over the probe phase's kernels."""
+def traffic_of(rec, names, optional=()):
+    """HBM bytes per launch summed over the probe phase's kernels (and those
+    of `optional` that ran)."""
     if not rec:
         return None
     ks = rec.get("kernels", {})
     tot = 0
-    for base in names:
+    for base in tuple(names) + tuple(b for b in optional if b in ks):
         k = ks.get(base)
         if not k:
             return None
@@ -386,14 +390,14 @@ def main():
         return round(b / (t_ms / 1000.0) / 1e9 / peak, 4) if t_ms > 0 else None
 
     roof = {
-        "scope": ("probe phase: S radix partition passes + k_join (SURVEY 8(d) t_probe)" if strategy == "radix"
+        "scope": ("probe phase: S radix partition passes + k_join_u (SURVEY 8(d) t_probe)" if strategy == "radix"
                   else "probe phase: k_probe + k_probe_slow (global table)"),
         "bound": "hbm",
         "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": frac(probe_bytes, probe_ms),
-        "traffic": traffic_of(rec, PROBE_KERNELS) if (strategy == "radix" and not use_dist) else None,
+        "traffic": traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS) if (strategy == "radix" and not use_dist) else None,
         "traffic_source": traffic_note,
         "algorithmic_bytes": probe_bytes,
         "bytes_per_probe_row": round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2),
@@ -403,11 +407,11 @@ def main():
     }
     if not use_dist and strategy == "radix":
         kbytes = (nr + ns) * (16 if wide else 8) + m_local * PAIR
-        roof["kernel"] = {"name": "k_join (hj_radix.hip)", "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
+        roof["kernel"] = {"name": "k_join_u (hj_radix.hip; + k_join over deferred items)",
+                          "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
                           if join_ms > 0 else None, "frac": frac(kbytes, join_ms),
                           "algorithmic_bytes_per_launch": kbytes, "avg_launch_ms": round(join_ms, 4),
-                          "traffic": (rec or {}).get("kernels", {}).get("k_join", {}).get("hbm_bytes_per_launch")
-                          if rec else None}
+                          "traffic": traffic_of(rec, ("k_join_u",)) if rec else None}
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),

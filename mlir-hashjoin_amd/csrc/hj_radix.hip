@@ -823,6 +823,11 @@ struct JoinArgs {
     long long cap;
     u64 *counter;
     u64 *dup_flag;                   // set to 1 if any partition's build rows repeat a key
+    // k_join_u appends the items it leaves (repeated / INT64_MIN build keys,
+    // build side over one round) to defer[0 .. *defer_n); k_join in list
+    // mode (list != nullptr) joins exactly those items
+    unsigned *defer = nullptr, *defer_n = nullptr;
+    const unsigned *list = nullptr, *list_n = nullptr;
 };
 
 struct ItemDesc {
@@ -833,8 +838,9 @@ struct ItemDesc {
 // (scalar) load instead of the owner -> partition -> offsets chain.
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
                                                    const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
-                                                   ItemDesc *desc) {
+                                                   ItemDesc *desc, unsigned *zero) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
+    if (w == 0 && zero) *zero = 0u;
     if (w >= work_start[P]) return;
     const int p = (int)work_owner[w];
     const unsigned c = w - work_start[p];
@@ -860,7 +866,7 @@ __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, c
 // PF: prefetch the next item's first R round and S sub-chunk into registers
 // while this item is probed (needs the register room of WPS = 2).
 template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems, int WPS = 4, int RCAPX = 0,
-          bool PF = false>
+          bool PF = false, bool LIST = false>
 __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -886,13 +892,17 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     constexpr int NW = NT / 64;
     __shared__ unsigned s_cw[SI * NW];        // per (row slot, wave) match counts, then offsets
 
-    const unsigned total = a.work_start[a.P];
+    const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
     unsigned w = blockIdx.x;
     if (w >= total) return;
     const T *rrows = (const T *)a.r;
     const T *srows = (const T *)a.s;
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
+    auto item = [&](unsigned x) {
+        if constexpr (LIST) return a.desc[a.list[x]];
+        else return a.desc[x];
+    };
 
     // Row slot i of wave v is run lo + i * NW + v, lane l its row l: the
     // run entry is wave-uniform (scalar loads into SGPRs) and can be
@@ -926,10 +936,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     unsigned rok = 0, sok = 0;   // bit i: rv_[i] / sv_[i] holds a row
     u64 er[RI], es[SI];
     bool dup_sent = false;   // this workgroup has set a.dup_flag
-    ItemDesc it = a.desc[w];
+    ItemDesc it = item(w);
     ents(a.r_runs, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
     ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
-    ItemDesc nx = a.desc[w + gridDim.x < total ? w + gridDim.x : w];
+    ItemDesc nx = item(w + gridDim.x < total ? w + gridDim.x : w);
     auto load_r = [&](u64 r0) {
         ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
         return rows_of(rrows, er, rv_, RI);
@@ -962,7 +972,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
         if (more) {
             ents(a.r_runs, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
             ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
-            if (w + 2 * gridDim.x < total) nnx = a.desc[w + 2 * gridDim.x];
+            if (w + 2 * gridDim.x < total) nnx = item(w + 2 * gridDim.x);
         }
 
         u64 n_null_r = 0;
@@ -1356,6 +1366,329 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     }
 }
 
+// --------------------------------------------------------------- join, fast path
+// k_join_u: the join of items whose partition holds no INT64_MIN build key
+// and at most rmax runs (load factor <= 0.75) -- every item of the PK-FK
+// and uniform-key configs.  Against k_join it drops the null pass, the
+// oversized-partition rounds that re-probe S, the paired duplicate walk
+// and the wave-cooperative writes, so it needs ~80 instead of ~127 VGPRs
+// and runs 768-thread workgroups at 6 waves per SIMD (k_join: 4).  An item
+// it cannot take is appended to a.defer (one atomic per such item, before
+// any of its pairs is written) and k_join joins the list afterwards.
+// Run entries, table, duplicate-free probe walk, ballot-compacted output
+// and the ONE cursor atomic per sub-chunk are as in k_join; a partition
+// with a repeated build key (GEN) takes a plain per-row walk to EMPTY.
+// Scalar (s_load) reads of wave-uniform words that no kernel writes while
+// the join runs: through the constant address space.  Plain pointers here
+// compile to vector loads whose results the allocator spilled, and each
+// spill's vmcnt(0) then waited for every row load in flight.
+typedef __attribute__((address_space(4))) const u64 cu64_t;
+__device__ __forceinline__ u64 sload(const u64 *p) { return *(cu64_t *)p; }
+__device__ __forceinline__ ItemDesc sload(const ItemDesc *p) {
+    const u64 *q = (const u64 *)p;
+    return ItemDesc{sload(q), sload(q + 1), sload(q + 2), sload(q + 3)};
+}
+
+template <bool WIDE, bool WRITE, int TSL, int NT, int RI, int SI, int WPS, bool GEN = true>
+__global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;
+    constexpr int TS = 1 << TSL;
+    constexpr unsigned kMask = TS - 1;
+    constexpr int NW = NT / 64;
+    constexpr unsigned rb = (unsigned)(NW * RI);    // runs per build round (RI per wave)
+    constexpr unsigned subb = (unsigned)(NW * SI);  // runs per sub-chunk
+    constexpr unsigned rmax = (unsigned)(TS * 3 / 4) >> kRunLog;   // build runs per table (load factor <= 0.75)
+    static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
+    constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
+    __shared__ u64 tkey[TS];
+    __shared__ u64 tpay[WIDE ? TS : 1];
+    __shared__ u64 s_base;
+    __shared__ unsigned s_bad, s_dup;
+    __shared__ unsigned s_cw[SI * NW];
+    __shared__ u64 wsum[16];
+    bool dup_sent = false;   // this workgroup has set a.dup_flag
+
+    const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
+    unsigned w = blockIdx.x;
+    if (w >= total) return;
+    const T *rrows = (const T *)a.r;
+    const T *srows = (const T *)a.s;
+    PT *orr = (PT *)a.out_r;
+    PT *oss = (PT *)a.out_s;
+    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
+    const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
+    const int lane = threadIdx.x & 63;
+    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const u64 li = lo + (u64)i * NW + wv0;
+            e[i] = li < hi ? sload(list + li) : 0ull;
+        }
+    };
+    // Every lane loads (a lane past its run's end re-reads the run's first
+    // row; no run: row 0), so the loads are straight-line code and the build
+    // waits for the R rows only (vmcnt(SI)), not for the S rows behind them.
+    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
+        unsigned ok = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const bool in = off < (unsigned)(e[i] & 127u);
+            v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + (in ? off : 0u));
+            ok |= (unsigned)in << i;
+        }
+        return ok;
+    };
+    T sv_[SI], rv_[RI];
+    u64 er[RI], es[SI];
+    ItemDesc it = sload(a.desc + w);
+    ents(a.r_runs, it.r_lo, it.r_hi, er, RI);
+    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    while (true) {
+        const bool fits = it.r_hi - it.r_lo <= (u64)rmax;   // uniform
+        unsigned rok = 0, sok = 0;
+        if (fits) {
+            rok = rows_of(rrows, er, rv_, RI);
+            sok = rows_of(srows, es, sv_, SI);
+        }
+        // the next item's descriptor and run entries (scalar loads): their
+        // latency passes while this item's rows are in flight
+        const bool more = w + gridDim.x < total;
+        u64 ner[RI], nes[SI];
+        ItemDesc nx = it;
+        if (more) {
+            nx = sload(a.desc + w + gridDim.x);
+            ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
+            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+        }
+        if (!fits) {
+            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+        } else {
+            for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
+            if (threadIdx.x == 0) s_bad = s_dup = 0u;
+            __syncthreads();
+            // ---- build: every row's first CAS issued before any result is
+            // used; a partition of more than rb runs (up to rmax) takes more
+            // rounds into the same table
+            bool bad = false, dup = false;
+            for (u64 r0 = it.r_lo;;) {
+            unsigned hb[RI];
+            u64 ob[RI], vb[RI];
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                const u64 key = R::key(rv_[i]);
+                bool act = (rok >> i) & 1u;
+                if (WIDE && act && key == kEmptyKey64) {   // the null pass lives in k_join
+                    bad = true;
+                    act = false;
+                }
+                hb[i] = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                if constexpr (WIDE) vb[i] = key;
+                else vb[i] = rv_[i];
+                ob[i] = act ? atomicCAS(&tkey[hb[i]], kEmpty, vb[i]) : kEmpty;
+                if (!act) rok &= ~(1u << i);
+            }
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                if (!((rok >> i) & 1u)) continue;
+                const u64 key = R::key(rv_[i]);
+                unsigned h = hb[i];
+                u64 old = ob[i];
+                while (old != kEmpty) {
+                    dup |= WIDE ? (old == key) : ((old >> 32) == key);
+                    h = (h + 1) & kMask;
+                    old = atomicCAS(&tkey[h], kEmpty, vb[i]);
+                }
+                if constexpr (WIDE) tpay[h] = R::pay(rv_[i]);
+            }
+            r0 += rb;
+            if (r0 >= it.r_hi) break;
+            ents(a.r_runs, r0, it.r_hi, er, RI);
+            rok = rows_of(rrows, er, rv_, RI);
+            }
+            if (bad || (!GEN && dup)) s_bad = 1u;
+            if (dup) s_dup = 1u;
+            __syncthreads();
+            const bool unique = s_dup == 0u;
+            if (!unique && !dup_sent) {   // once per workgroup (k_join)
+                if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dup_sent = true;
+            }
+            if (s_bad) {
+                if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            } else {
+                // ---- probe the chunk, one sub-chunk of S rows at a time
+                for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+                    if (sb != it.s_lo) {
+                        ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
+                        sok = rows_of(srows, es, sv_, SI);
+                    }
+                    // an INT64_MIN probe key matches nothing here: the
+                    // partition has no null build row (else deferred)
+                    unsigned pm = 0u;   // bit i: row slot i probes
+#pragma unroll
+                    for (int i = 0; i < SI; ++i)
+                        if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64)) pm |= 1u << i;
+                    if (GEN && !unique) {
+                        // a repeated build key: every row walks its chain to
+                        // EMPTY, counting, then again writing at its prefix
+                        unsigned cnt = 0, mb = 0u;   // mb bit i: row slot i has a match
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            if (!((pm >> i) & 1u)) continue;
+                            const u64 key = R::key(sv_[i]);
+                            unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                            u64 e = tkey[h];
+                            const unsigned c0 = cnt;
+                            while (e != kEmpty) {
+                                if ((WIDE ? e : (e >> 32)) == key) ++cnt;
+                                h = (h + 1) & kMask;
+                                e = tkey[h];
+                            }
+                            if (cnt != c0) mb |= 1u << i;
+                        }
+                        u64 tot;
+                        const u64 pre = block_excl_scan<NT>((u64)cnt, wsum, &tot);
+                        if (!WIDE && WRITE && sb == it.s_lo && tot > (u64)(2 * NT * SI)) {
+                            // many pairs per probe row (the reference's 10M x 10M
+                            // keys in [1, 100k]): one lane per row would store
+                            // one partial line per pair; k_join's wave-cooperative
+                            // writes take the item (nothing of it written yet)
+                            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+                            break;
+                        }
+                        if constexpr (!WRITE) {
+                            if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                        } else if (tot) {
+                            if (threadIdx.x == 0) s_base = atomicAdd(a.counter, tot);
+                            __syncthreads();
+                            u64 pos = s_base + pre;
+#pragma unroll
+                            for (int i = 0; i < SI; ++i) {
+                                if (!((mb >> i) & 1u)) continue;
+                                const u64 key = R::key(sv_[i]);
+                                const PT spay = (PT)R::pay(sv_[i]);
+                                unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
+                                u64 e = tkey[h];
+                                while (e != kEmpty) {
+                                    if ((WIDE ? e : (e >> 32)) == key) {
+                                        if (pos < (u64)a.cap) {
+                                            orr[pos] = WIDE ? (PT)tpay[h] : (PT)(e & 0xffffffffull);
+                                            oss[pos] = spay;
+                                        }
+                                        ++pos;
+                                    }
+                                    h = (h + 1) & kMask;
+                                    e = tkey[h];
+                                }
+                            }
+                        }
+                        __syncthreads();   // s_base reused by the next sub-chunk
+                        continue;
+                    }
+                    // first slot of every row read before any is resolved
+                    unsigned m[SI], hp[SI];
+                    u64 e0[SI];
+                    bool pa[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        m[i] = 0xFFFFFFFFu;
+                        pa[i] = (pm >> i) & 1u;
+                        hp[i] = (unsigned)(rhash(R::key(sv_[i])) >> a.tshift) & kMask;
+                        e0[i] = pa[i] ? tkey[hp[i]] : kEmpty;
+                    }
+                    auto open = [&](u64 e, u64 key) { return e != kEmpty && (WIDE ? e : (e >> 32)) != key; };
+#pragma unroll
+                    for (int i = 0; i < SI; i += 2) {
+                        const int j = i + 1 < SI ? i + 1 : i;
+                        const u64 ka = R::key(sv_[i]), kb = R::key(sv_[j]);
+                        unsigned ha = hp[i], hb2 = hp[j];
+                        u64 ea = e0[i], eb = e0[j];
+                        bool la = pa[i] && open(ea, ka);
+                        bool lb = j != i && pa[j] && open(eb, kb);
+                        while (la || lb) {
+                            if (la) {
+                                ha = (ha + 1) & kMask;
+                                ea = tkey[ha];
+                            }
+                            if (lb) {
+                                hb2 = (hb2 + 1) & kMask;
+                                eb = tkey[hb2];
+                            }
+                            la = la && open(ea, ka);
+                            lb = lb && open(eb, kb);
+                        }
+                        if (pa[i] && ea != kEmpty && (WIDE ? ea : (ea >> 32)) == ka) m[i] = ha;
+                        if (j != i && pa[j] && eb != kEmpty && (WIDE ? eb : (eb >> 32)) == kb) m[j] = hb2;
+                    }
+                    // <= 1 match per row: ballot compaction in row-slot-major
+                    // order (one coalesced run per wave and slot)
+                    const int wv = threadIdx.x >> 6;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 bal = __ballot(m[i] != 0xFFFFFFFFu);
+                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                    }
+                    __syncthreads();
+                    if (wv == 0) {   // exclusive scan of the SI * NW run lengths
+                        constexpr int K = (SI * NW + 63) / 64;
+                        unsigned v[K], sum = 0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int jj = lane * K + k;
+                            v[k] = jj < SI * NW ? s_cw[jj] : 0u;
+                            sum += v[k];
+                        }
+                        unsigned x = sum;
+#pragma unroll
+                        for (int o = 1; o < 64; o <<= 1) {
+                            const unsigned y = __shfl_up(x, o, 64);
+                            if (lane >= o) x += y;
+                        }
+                        unsigned run = x - sum;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int jj = lane * K + k;
+                            if (jj < SI * NW) s_cw[jj] = run;
+                            run += v[k];
+                        }
+                        if (lane == 63 && x) {
+                            if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
+                            else atomicAdd(a.counter, (u64)x);
+                        }
+                    }
+                    if constexpr (WRITE) {
+                        __syncthreads();
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            // the lane's rank among the wave's matches of row slot i
+                            // (ballot again rather than keep SI ranks live across the barrier)
+                            const u64 bal = __ballot(m[i] != 0xFFFFFFFFu);
+                            if (m[i] == 0xFFFFFFFFu) continue;
+                            const u64 pos = s_base + s_cw[i * NW + wv] + (unsigned)__popcll(bal & lt);
+                            if (pos < (u64)a.cap) {
+                                st_s<kNtJoinSt>(orr + pos, WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull));
+                                st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
+                            }
+                        }
+                    }
+                    __syncthreads();   // s_cw / s_base reused by the next sub-chunk
+                }
+            }
+            __syncthreads();   // table reused by the next item
+        }
+        if (!more) break;
+        w += gridDim.x;
+        it = nx;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) er[i] = ner[i];
+#pragma unroll
+        for (int i = 0; i < SI; ++i) es[i] = nes[i];
+    }
+}
+
 // --------------------------------------------------------------- bucketized join
 // k_join2: the same work items as k_join, but the partition's LDS table is
 // BUCKETIZED and holds no keys:
@@ -1701,15 +2034,19 @@ __global__ __launch_bounds__(NT, 4) void k_join2(JoinArgs a) {
 }
 
 
-// Join kernel variant: log2 LDS slots and workgroup size.  HJ_JOIN_TSL
-// (11 | 12 | 13) overrides the default for experiments.  HJ_JOIN=2 selects
-// the bucketized k_join2 (measured slower: profiles/r02_micro_join_bucketized.txt).
+// Join kernel variant.  Default (kind 0): k_join_u, 768 threads, 3 build +
+// 3 probe rows per thread, 6 waves per SIMD, with k_join over the items it
+// defers (profiles/r02_join_fast.txt: C3 k_join 3.50 -> 2.81 ms, C2 12.34 ->
+// 9.45 ms, C1-ref 1.31 -> 0.96 ms).  HJ_JOIN=1 runs k_join alone (HJ_JOIN_TSL
+// 11 | 12 | 13 picks its table), HJ_JOIN=2 the bucketized k_join2, 3 / 4
+// k_join's register-prefetch variants (all measured slower: DESIGN.md 4).
 struct JoinVariant {
     int tsl;
     int nt;
-    int kind;   // 1 k_join, 2 k_join2
+    int kind;   // 0 k_join_u + k_join, 1 k_join, 2 k_join2, 3 / 4 prefetching k_join
     int si;     // S rows per thread per sub-chunk
 };
+constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 JoinVariant join_variant() {
     static int tsl = [] {
         const char *e = getenv("HJ_JOIN_TSL");
@@ -1718,9 +2055,10 @@ JoinVariant join_variant() {
     }();
     static int kind = [] {
         const char *e = getenv("HJ_JOIN");
-        const int v = e ? atoi(e) : 1;
-        return (v >= 1 && v <= 4) ? v : 1;
+        const int v = e ? atoi(e) : 0;
+        return (v >= 0 && v <= 4) ? v : 0;
     }();
+    if (kind == 0) return JoinVariant{12, kFastNT, 0, kFastSI};
     if (kind == 2) return JoinVariant{12, 512, 2, kJ2SI};
     if (kind == 3) return JoinVariant{13, 512, 3, 5};   // prefetching k_join, 1 workgroup per CU, 8192 slots
     if (kind == 4) return JoinVariant{12, 512, 4, 3};   // prefetching k_join, 2 workgroups per CU, 3 S rows
@@ -1941,7 +2279,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     const JoinVariant jv = join_variant();
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
     // persistent grid: as many workgroups as fit at once (LDS-limited)
-    const int per_cu = jv.kind == 2 || jv.kind == 4 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
+    const int per_cu = jv.kind == 0 || jv.kind == 2 || jv.kind == 4 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
     const unsigned pg = (unsigned)(per_cu * cu_count());
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
@@ -1952,9 +2290,12 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     if (want > chb) chb = (want + subb - 1) / subb * subb;
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
+    // fast path: the deferred-item list lives after the work map
+    const bool fast = jv.kind == 0;
+    unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc);
+                       (ItemDesc *)desc, fast ? defer_n : nullptr);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -1984,6 +2325,34 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     hipLaunchKernelGGL((k_join2<W, WR, kJ2NT, kJ2RI, kJ2NBL, kJ2SI>), dim3(grid), dim3(kJ2NT), 0, st, a)
 #define HJ_JOINP(W, WR, TSL, SI, WPS)                                                                        \
     hipLaunchKernelGGL((k_join<W, WR, TSL, 512, 0, SI, WPS, 2560, true>), dim3(grid), dim3(512), 0, st, a)
+#define HJ_JOINU(W, WR) \
+    hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid), dim3(kFastNT), 0, st, a)
+    if (fast) {
+        a.defer = defer_n + 1;
+        a.defer_n = defer_n;
+        if (wide) {
+            if (count_only) HJ_JOINU(true, false);
+            else HJ_JOINU(true, true);
+        } else {
+            if (count_only) HJ_JOINU(false, false);
+            else HJ_JOINU(false, true);
+        }
+        // the items it left, by the general kernel (a persistent grid that
+        // exits at once when the list is empty)
+        a.list = defer_n + 1;
+        a.list_n = defer_n;
+#define HJ_JOINL(W, WR) \
+    hipLaunchKernelGGL((k_join<W, WR, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512), 0, st, a)
+        if (wide) {
+            if (count_only) HJ_JOINL(true, false);
+            else HJ_JOINL(true, true);
+        } else {
+            if (count_only) HJ_JOINL(false, false);
+            else HJ_JOINL(false, true);
+        }
+#undef HJ_JOINL
+        return hipGetLastError();
+    }
     if (jv.kind == 3 || jv.kind == 4) {
         if (jv.kind == 3) {
             if (wide) {
@@ -2018,6 +2387,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         else HJ_JOIN_V(false, true);
     }
 #undef HJ_JOINP
+#undef HJ_JOINU
 #undef HJ_JOIN2
 #undef HJ_JOIN_V
 #undef HJ_JOIN
