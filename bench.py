@@ -258,6 +258,11 @@ def host_leg(hashjoin, seed):
 
 def main():
     a = parse()
+    # stdout carries exactly ONE JSON line: everything else written to fd 1
+    # (RCCL's init banner, library chatter) goes to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -459,7 +464,7 @@ def main():
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     hj.close()
     if use_dist:
         dist.destroy_process_group()

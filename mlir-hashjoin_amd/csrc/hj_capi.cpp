@@ -156,6 +156,16 @@ struct hj_ctx {
         int64_t m = 0;
     } memo;
     long long memo_hits = 0;
+    // radix join kernel choice: the fast path (k_join_u) defers items it
+    // cannot take to k_join; the list-mode launch leaves {deferred, items}
+    // in join_stats (host-mapped).  When the last fast join deferred most of
+    // its items (keys that mostly repeat: the reference's 10M x 10M keys in
+    // [1, 100k]), the next joins skip the fast path, re-checking it every
+    // kFastRecheck joins.
+    unsigned *join_stats = nullptr;       // host-mapped pinned, 2 words
+    unsigned *join_stats_dev = nullptr;
+    unsigned long long joins = 0;
+    static constexpr unsigned kFastRecheck = 8;
 };
 
 namespace {
@@ -394,9 +404,23 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
+        if (!c->join_stats) {
+            void *hp = nullptr;
+            HJ_HIP(hipHostMalloc(&hp, 2 * sizeof(unsigned), hipHostMallocMapped));
+            c->join_stats = (unsigned *)hp;
+            c->join_stats[0] = c->join_stats[1] = 0u;
+            void *dp = nullptr;
+            HJ_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+            c->join_stats_dev = (unsigned *)dp;
+        }
+        // (read without waiting: the values of whichever fast join finished last)
+        const unsigned deferred = ((volatile unsigned *)c->join_stats)[0];
+        const unsigned items = ((volatile unsigned *)c->join_stats)[1];
+        const bool general = items > 0 && 2ull * deferred > items && (c->joins % hj_ctx::kFastRecheck) != 0;
+        ++c->joins;
         HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
-                              (unsigned long long *)d_count, c->meta + 1, count_only, st));
+                              (unsigned long long *)d_count, c->meta + 1, count_only, st, c->join_stats_dev, general));
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
@@ -910,6 +934,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->side) (void)hipFree(c->side);
     if (c->meta) (void)hipFree(c->meta);
     if (c->dcount) (void)hipFree(c->dcount);
+    if (c->join_stats) (void)hipHostFree(c->join_stats);
     for (int i = 0; i < hj_ctx::kDbufs; ++i)
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);

@@ -828,6 +828,7 @@ struct JoinArgs {
     // mode (list != nullptr) joins exactly those items
     unsigned *defer = nullptr, *defer_n = nullptr;
     const unsigned *list = nullptr, *list_n = nullptr;
+    unsigned *stats = nullptr;       // list mode: {deferred items, items} for the caller's next choice
 };
 
 struct ItemDesc {
@@ -893,6 +894,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     __shared__ unsigned s_cw[SI * NW];        // per (row slot, wave) match counts, then offsets
 
     const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
+    if (LIST && a.stats && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.stats[0] = total;
+        a.stats[1] = a.work_start[a.P];
+    }
     unsigned w = blockIdx.x;
     if (w >= total) return;
     const T *rrows = (const T *)a.r;
@@ -1472,7 +1477,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
             // ---- build: every row's first CAS issued before any result is
             // used; a partition of more than rb runs (up to rmax) takes more
             // rounds into the same table
-            bool bad = false, dup = false;
+            bool bad = false;
+            unsigned ndup = 0;   // this thread's rows whose CAS walk met their own key
             for (u64 r0 = it.r_lo;;) {
             unsigned hb[RI];
             u64 ob[RI], vb[RI];
@@ -1496,11 +1502,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                 const u64 key = R::key(rv_[i]);
                 unsigned h = hb[i];
                 u64 old = ob[i];
+                bool d = false;
                 while (old != kEmpty) {
-                    dup |= WIDE ? (old == key) : ((old >> 32) == key);
+                    d |= WIDE ? (old == key) : ((old >> 32) == key);
                     h = (h + 1) & kMask;
                     old = atomicCAS(&tkey[h], kEmpty, vb[i]);
                 }
+                ndup += d ? 1u : 0u;
                 if constexpr (WIDE) tpay[h] = R::pay(rv_[i]);
             }
             r0 += rb;
@@ -1508,15 +1516,20 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
             ents(a.r_runs, r0, it.r_hi, er, RI);
             rok = rows_of(rrows, er, rv_, RI);
             }
-            if (bad || (!GEN && dup)) s_bad = 1u;
-            if (dup) s_dup = 1u;
+            if (bad || (!GEN && ndup)) s_bad = 1u;
+            if (ndup) atomicAdd(&s_dup, ndup);
             __syncthreads();
-            const bool unique = s_dup == 0u;
+            const unsigned nd = s_dup;
+            const bool unique = nd == 0u;
+            // i32 rows whose keys mostly repeat (the reference's 10M x 10M keys
+            // in [1, 100k]: ~100 copies each) produce many pairs per probe row:
+            // k_join's wave-cooperative writes take them, before any probe
+            const bool defer_it = s_bad || (!WIDE && WRITE && (u64)nd * 4u > (it.r_hi - it.r_lo) << kRunLog);
             if (!unique && !dup_sent) {   // once per workgroup (k_join)
                 if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 dup_sent = true;
             }
-            if (s_bad) {
+            if (defer_it) {
                 if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             } else {
                 // ---- probe the chunk, one sub-chunk of S rows at a time
@@ -2273,7 +2286,8 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
 
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
-                      unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st) {
+                      unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
+                      unsigned *join_stats, bool general) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     const JoinVariant jv = join_variant();
@@ -2291,7 +2305,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
     // fast path: the deferred-item list lives after the work map
-    const bool fast = jv.kind == 0;
+    const bool fast = jv.kind == 0 && !general;
     unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
@@ -2341,6 +2355,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         // exits at once when the list is empty)
         a.list = defer_n + 1;
         a.list_n = defer_n;
+        a.stats = join_stats;
 #define HJ_JOINL(W, WR) \
     hipLaunchKernelGGL((k_join<W, WR, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512), 0, st, a)
         if (wide) {

@@ -250,3 +250,31 @@ def test_radix_i32_many_matches_per_row(hj, oracle, bits):
     exp = oracle.chained_join_i32(r, s, H=400)
     assert len(o[0]) == len(exp[0]) > 2 * len(s)
     assert oracle.same_multiset(*o, exp[0].astype(np.int64), exp[1].astype(np.int64))
+
+
+def test_fast_path_switch_repeated_joins(oracle):
+    """Join-kernel choice across repeated joins on one context: a join whose
+    items the fast path (k_join_u) mostly defers (i32 keys that repeat ~40x,
+    the reference's REF-A shape) makes the following joins run k_join alone,
+    re-checking the fast path every 8th join; a duplicate-free join in
+    between runs the fast path again.  Every join must equal the oracle."""
+    h = HashJoin(0)
+    try:
+        h.set_strategy("radix", radix_bits=6)
+        rk = oracle.gen_uniform_i64(7, 1, 1, 400, 16000)[0].astype(np.int32)
+        sk = oracle.gen_uniform_i64(7, 2, 1, 400, 12000)[0].astype(np.int32)
+        exp = oracle.chained_join_i32(rk, sk, H=64)
+        pk_r, pk_p, pk_s, pk_sp = oracle.gen_pkfk_i64(6, 20000, 30000, 0.9)
+        exp_pk = oracle.chained_join_i64(pk_r, pk_p, pk_s, pk_sp, H=200)
+        for i in range(18):
+            if i == 9:   # a duplicate-free i64 join in the middle of the run
+                o_r, o_s = h.join(dev(pk_r), dev(pk_p), dev(pk_s), dev(pk_sp))
+                torch.cuda.synchronize()
+                assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp_pk), f"join {i}"
+                continue
+            o_r, o_s = h.join(dev(rk), None, dev(sk), None)
+            torch.cuda.synchronize()
+            assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
+                                        *exp), f"join {i}"
+    finally:
+        h.close()
