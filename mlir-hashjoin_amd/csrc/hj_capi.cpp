@@ -420,7 +420,8 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         ++c->joins;
         HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
-                              (unsigned long long *)d_count, c->meta + 1, count_only, st, c->join_stats_dev, general));
+                              (unsigned long long *)d_count, c->meta + 1, count_only, st, c->join_stats_dev, general,
+                              src.n >= 8 * c->n_build));
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;

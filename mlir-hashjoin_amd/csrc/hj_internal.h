@@ -140,11 +140,12 @@ size_t radix_item_desc_bytes();
 // join_stats (host-mapped, 2 words, may be null): the join leaves there
 // {items deferred by the fast path, items}; general = skip the fast path
 // (k_join over every item), chosen by the caller when the last join on the
-// context deferred most of its items.
+// context deferred most of its items; stream = the probe side is many times
+// the build side (C2): the fast path's larger-sub-chunk shape.
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats = nullptr, bool general = false);
+                      unsigned *join_stats = nullptr, bool general = false, bool stream = false);
 
 // Routing fan-out limit: k_part_scatter (> 512 parts) keeps 12 B of LDS
 // counters per part, k_part_hist 4 B (<= 96 KiB of the 160 KiB).

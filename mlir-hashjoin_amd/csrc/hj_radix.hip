@@ -2060,6 +2060,11 @@ struct JoinVariant {
     int si;     // S rows per thread per sub-chunk
 };
 constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
+// probe sides much larger than the build side (C2: 2^30 x 2^20, ~1000 S rows
+// per R row): many sub-chunks per item, so bigger sub-chunks and more waves
+// (1024 threads x 4 S rows, 8 waves per SIMD): C2 join 9.45 -> 8.77 ms, C3
+// 2.79 -> 3.32 ms (profiles/r02_join_shapes.txt)
+constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
 JoinVariant join_variant() {
     static int tsl = [] {
         const char *e = getenv("HJ_JOIN_TSL");
@@ -2287,7 +2292,7 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats, bool general) {
+                      unsigned *join_stats, bool general, bool stream) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     const JoinVariant jv = join_variant();
@@ -2298,14 +2303,16 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
     // long as ~16 items per workgroup remain for balance
-    const unsigned subb = (unsigned)((jv.nt * jv.si) >> kRunLog);
+    const bool fast = jv.kind == 0 && !general;
+    const bool stream_shape = fast && stream;
+    const unsigned subb = stream_shape ? (unsigned)((kStreamNT * kStreamSI) >> kRunLog)
+                                       : (unsigned)((jv.nt * jv.si) >> kRunLog);
     u64 chb = (u64)kJoinSub * subb;
     const u64 want = (u64)s_runs / (16ull * pg);
     if (want > chb) chb = (want + subb - 1) / subb * subb;
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
     // fast path: the deferred-item list lives after the work map
-    const bool fast = jv.kind == 0 && !general;
     unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
@@ -2339,8 +2346,15 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     hipLaunchKernelGGL((k_join2<W, WR, kJ2NT, kJ2RI, kJ2NBL, kJ2SI>), dim3(grid), dim3(kJ2NT), 0, st, a)
 #define HJ_JOINP(W, WR, TSL, SI, WPS)                                                                        \
     hipLaunchKernelGGL((k_join<W, WR, TSL, 512, 0, SI, WPS, 2560, true>), dim3(grid), dim3(512), 0, st, a)
-#define HJ_JOINU(W, WR) \
-    hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid), dim3(kFastNT), 0, st, a)
+#define HJ_JOINU(W, WR)                                                                                    \
+    do {                                                                                                   \
+        if (stream_shape)                                                                                  \
+            hipLaunchKernelGGL((k_join_u<W, WR, 12, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), dim3(grid), \
+                               dim3(kStreamNT), 0, st, a);                                                 \
+        else                                                                                               \
+            hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),      \
+                               dim3(kFastNT), 0, st, a);                                                   \
+    } while (0)
     if (fast) {
         a.defer = defer_n + 1;
         a.defer_n = defer_n;

@@ -278,3 +278,16 @@ def test_fast_path_switch_repeated_joins(oracle):
                                         *exp), f"join {i}"
     finally:
         h.close()
+
+
+@pytest.mark.parametrize("dist", ["pkfk", "dups"])
+def test_radix_probe_heavy_stream_shape(hj, oracle, dist):
+    """A probe side >= 8x the build side takes the fast join's stream shape
+    (1024 threads, 4 probe rows per thread, many sub-chunks per item)."""
+    if dist == "pkfk":
+        rk, rp, sk, sp = oracle.gen_pkfk_i64(11, 6000, 90000, 0.8)
+    else:
+        rk, rp = oracle.gen_uniform_i64(11, 1, 1, 3000, 6000)
+        sk, sp = oracle.gen_uniform_i64(11, 2, 1, 3000, 90000)
+    o = run(hj, rk, rp, sk, sp, 3)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=300))
