@@ -1404,13 +1404,19 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     constexpr int NW = NT / 64;
     constexpr unsigned rb = (unsigned)(NW * RI);    // runs per build round (RI per wave)
     constexpr unsigned subb = (unsigned)(NW * SI);  // runs per sub-chunk
-    constexpr unsigned rmax = (unsigned)(TS * 3 / 4) >> kRunLog;   // build runs per table (load factor <= 0.75)
+    // A partition's runs may be partly filled (a small build side partitioned
+    // by many workgroups: C2's 2^20 rows, ~32-50 runs of ~2048 rows), so the
+    // table takes up to TS / 64 runs (<= TS rows: every insert walk ends) and
+    // the item is deferred when the rows counted during the build exceed
+    // rmax_rows (load factor 0.75).
+    constexpr unsigned rmax = (unsigned)TS >> kRunLog;
+    constexpr unsigned rmax_rows = (unsigned)(TS * 3 / 4);
     static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
     constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
     __shared__ u64 tkey[TS];
     __shared__ u64 tpay[WIDE ? TS : 1];
     __shared__ u64 s_base;
-    __shared__ unsigned s_bad, s_dup;
+    __shared__ unsigned s_bad, s_dup, s_rows;
     __shared__ unsigned s_cw[SI * NW];
     __shared__ u64 wsum[16];
     bool dup_sent = false;   // this workgroup has set a.dup_flag
@@ -1472,7 +1478,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
             if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
         } else {
             for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)tkey)[j] = make_ulonglong2(kEmpty, kEmpty);
-            if (threadIdx.x == 0) s_bad = s_dup = 0u;
+            if (threadIdx.x == 0) s_bad = s_dup = s_rows = 0u;
             __syncthreads();
             // ---- build: every row's first CAS issued before any result is
             // used; a partition of more than rb runs (up to rmax) takes more
@@ -1495,6 +1501,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                 else vb[i] = rv_[i];
                 ob[i] = act ? atomicCAS(&tkey[hb[i]], kEmpty, vb[i]) : kEmpty;
                 if (!act) rok &= ~(1u << i);
+            }
+            {   // the round's inserted rows, counted per wave (ballots: no VGPRs)
+                unsigned wn = 0;
+#pragma unroll
+                for (int i = 0; i < RI; ++i) wn += (unsigned)__popcll(__ballot((rok >> i) & 1u));
+                // the wave whose rows push the table past rmax_rows defers the item
+                if (lane == 0 && wn && atomicAdd(&s_rows, wn) + wn > rmax_rows) s_bad = 1u;
             }
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
@@ -1524,7 +1537,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
             // i32 rows whose keys mostly repeat (the reference's 10M x 10M keys
             // in [1, 100k]: ~100 copies each) produce many pairs per probe row:
             // k_join's wave-cooperative writes take them, before any probe
-            const bool defer_it = s_bad || (!WIDE && WRITE && (u64)nd * 4u > (it.r_hi - it.r_lo) << kRunLog);
+            const bool defer_it = s_bad ||
+                                  (!WIDE && WRITE && (u64)nd * 4u > (it.r_hi - it.r_lo) << kRunLog);
             if (!unique && !dup_sent) {   // once per workgroup (k_join)
                 if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 dup_sent = true;
@@ -2348,10 +2362,14 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     hipLaunchKernelGGL((k_join<W, WR, TSL, 512, 0, SI, WPS, 2560, true>), dim3(grid), dim3(512), 0, st, a)
 #define HJ_JOINU(W, WR)                                                                                    \
     do {                                                                                                   \
-        if (stream_shape)                                                                                  \
-            hipLaunchKernelGGL((k_join_u<W, WR, 12, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), dim3(grid), \
-                               dim3(kStreamNT), 0, st, a);                                                 \
-        else                                                                                               \
+        bool st_ = false;                                                                                  \
+        if constexpr (W) st_ = stream_shape;   /* (i32 rows: the fast shape only) */                     \
+        if constexpr (W) {                                                                                 \
+            if (st_)                                                                                       \
+                hipLaunchKernelGGL((k_join_u<true, WR, 12, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),   \
+                                   dim3(grid), dim3(kStreamNT), 0, st, a);                                 \
+        }                                                                                                  \
+        if (!st_)                                                                                          \
             hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),      \
                                dim3(kFastNT), 0, st, a);                                                   \
     } while (0)
