@@ -1701,7 +1701,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                             }
                         }
                     }
-                    __syncthreads();   // s_cw / s_base reused by the next sub-chunk
+                    // s_cw / s_base reused by the next sub-chunk (after the
+                    // last one, the table barrier below covers them)
+                    if (sb + subb < it.s_hi) __syncthreads();
                 }
             }
             __syncthreads();   // table reused by the next item
