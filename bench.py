@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--radix-bits", type=int, default=0)
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU code path (partition + all-to-all) even at N=1")
+    ap.add_argument("--log2", type=int, default=0,
+                    help="experiments: |R| = |S| = 2^LOG2 rows instead of the config's sizes (not a bench line)")
     return ap.parse_args()
 
 
@@ -279,6 +281,9 @@ def main():
     from hashjoin.dist import distributed_join
 
     NR, NS, distn, ktype, desc = CONFIGS[a.config]
+    if a.log2:
+        NR = NS = 1 << a.log2
+        desc = f"{desc} (resized: |R|=|S|=2^{a.log2})"
     wide = ktype == "int64"
     if use_dist and not wide:
         raise SystemExit("the multi-GPU path joins int64 key/payload columns")
