@@ -28,6 +28,47 @@ namespace hj {
 constexpr unsigned long long kEmptyKey64 = 0x8000000000000000ull;
 constexpr unsigned long long kEmptySlot32 = ~0ull;
 
+// Wave64 scans by DPP: row shifts 1, 2, 4, 8 inside each row of 16 lanes,
+// then row broadcasts of lane 15 (into rows 1, 3) and lane 31 (into rows 2,
+// 3).  A handful of VALU cycles per step, where __shfl_up / __shfl_xor are a
+// ds_bpermute (an LDS round trip) each; a wave scanning alone on a
+// workgroup's critical path (the partition pass's bin scan, the join's
+// output claim) waits for six of them in a row (micro/dpp_micro.hip).
+// A lane a DPP step reads from outside the row / mask contributes 0.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_or0(unsigned x) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned long long dpp_or0(unsigned long long x) {
+    const unsigned lo = dpp_or0<CTRL, ROWS>((unsigned)x), hi = dpp_or0<CTRL, ROWS>((unsigned)(x >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+// inclusive prefix sum over the wave's 64 lanes (all lanes active)
+template <typename T>
+__device__ __forceinline__ T wave_incl_add_t(T x) {
+    x += dpp_or0<0x111, 0xf>(x);   // row_shr:1
+    x += dpp_or0<0x112, 0xf>(x);   // row_shr:2
+    x += dpp_or0<0x114, 0xf>(x);   // row_shr:4
+    x += dpp_or0<0x118, 0xf>(x);   // row_shr:8
+    x += dpp_or0<0x142, 0xa>(x);   // row_bcast:15
+    x += dpp_or0<0x143, 0xc>(x);   // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ unsigned wave_incl_add(unsigned x) { return wave_incl_add_t(x); }
+__device__ __forceinline__ unsigned long long wave_incl_add64(unsigned long long x) { return wave_incl_add_t(x); }
+// maximum over the wave's 64 lanes, in every lane (all lanes active)
+__device__ __forceinline__ unsigned wave_max_all(unsigned x) {
+    auto mx = [](unsigned a, unsigned b) { return a > b ? a : b; };
+    x = mx(x, dpp_or0<0x111, 0xf>(x));
+    x = mx(x, dpp_or0<0x112, 0xf>(x));
+    x = mx(x, dpp_or0<0x114, 0xf>(x));
+    x = mx(x, dpp_or0<0x118, 0xf>(x));
+    x = mx(x, dpp_or0<0x142, 0xa>(x));
+    x = mx(x, dpp_or0<0x143, 0xc>(x));
+    return (unsigned)__builtin_amdgcn_readlane((int)x, 63);
+}
+
 struct alignas(16) Slot64 {
     unsigned long long key;
     unsigned long long pay;

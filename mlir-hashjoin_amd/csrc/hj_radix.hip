@@ -133,21 +133,11 @@ template <int NT>
 __device__ __forceinline__ u64 block_excl_scan(u64 v, u64 *wsum, u64 *total) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    u64 x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const u64 y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const u64 x = wave_incl_add64(v);
     if (lane == 63) wsum[w] = x;
     __syncthreads();
     if (w == 0) {
-        u64 t = lane < NW ? wsum[lane] : 0ull;
-#pragma unroll
-        for (int o = 1; o < NW; o <<= 1) {
-            const u64 y = __shfl_up(t, o, 64);
-            if (lane >= o) t += y;
-        }
+        const u64 t = wave_incl_add64(lane < NW ? wsum[lane] : 0ull);
         if (lane < NW) wsum[lane] = t;
     }
     __syncthreads();
@@ -573,22 +563,10 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
                     const unsigned y = (c[j] << 16) | (lane * 8u + j);
                     mx = y > mx ? y : mx;
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const unsigned y = (unsigned)__shfl_xor((int)mx, o, 64);
-                    mx = y > mx ? y : mx;
-                }
+                mx = wave_max_all(mx);
                 if (lane == 0) s_hot = (mx >> 16) > (unsigned)(kTile / 8) ? (mx & 0xffffu) : 0xFFFFFFFFu;
             }
-            unsigned x = s, xk = sk;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned y = __shfl_up(x, o, 64), yk = __shfl_up(xk, o, 64);
-                if (lane >= o) {
-                    x += y;
-                    xk += yk;
-                }
-            }
+            const unsigned x = wave_incl_add(s), xk = wave_incl_add(sk);
             unsigned run = x - s, runk = xk - sk;
             unsigned sv[8], nv[8];
 #pragma unroll
@@ -1194,12 +1172,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
                             v[k] = j < SI * NW ? s_cw[j] : 0u;
                             sum += v[k];
                         }
-                        unsigned x = sum;
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const unsigned y = __shfl_up(x, o, 64);
-                            if (lane >= o) x += y;
-                        }
+                        const unsigned x = wave_incl_add(sum);
                         unsigned run = x - sum;
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
@@ -1668,12 +1641,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                             v[k] = jj < SI * NW ? s_cw[jj] : 0u;
                             sum += v[k];
                         }
-                        unsigned x = sum;
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const unsigned y = __shfl_up(x, o, 64);
-                            if (lane >= o) x += y;
-                        }
+                        const unsigned x = wave_incl_add(sum);
                         unsigned run = x - sum;
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
@@ -1981,12 +1949,7 @@ __global__ __launch_bounds__(NT, 4) void k_join2(JoinArgs a) {
                             v[k] = j < SI * NW ? s_cw[j] : 0u;
                             sum += v[k];
                         }
-                        unsigned x = sum;
-#pragma unroll
-                        for (int o = 1; o < 64; o <<= 1) {
-                            const unsigned y = __shfl_up(x, o, 64);
-                            if (lane >= o) x += y;
-                        }
+                        const unsigned x = wave_incl_add(sum);
                         unsigned run = x - sum;
 #pragma unroll
                         for (int k = 0; k < K; ++k) {

@@ -78,10 +78,10 @@ int main(int argc, char **argv) {
         ms /= 5;
         printf("%-40s %7.3f ms  %7.1f GB/s (32 B/row)\n", name, ms, 32.0 * n / ms / 1e6);
     };
-    for (int fb : {9}) {
+    for (int fb : {8, 9}) {
         a.fbits = fb;
         a.shift = 64 - fb;
-        for (int pbl : {9}) {
+        for (int pbl : {9, 10}) {
             a.out_pbl = pbl;
             char nm[64];
             snprintf(nm, sizeof nm, "F%d PB%d k_pass", 1 << fb, 1 << pbl);
