@@ -170,7 +170,7 @@ def cpu_baseline(seed, log2n):
 # ---------------------------------------------------------------- roofline helpers
 def kernel_source_sha():
     h = hashlib.sha256()
-    for f in ("hj_radix.hip", "hj_kernels.hip"):
+    for f in ("hj_radix.hip", "hj_kernels.hip", "hj_internal.h", "hj_gen.h"):
         with open(os.path.join(ROOT, "mlir-hashjoin_amd", "csrc", f), "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
