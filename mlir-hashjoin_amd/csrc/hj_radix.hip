@@ -1214,23 +1214,27 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
                         // store.  Instead the wave takes its rows one at a time
                         // and scans the row's chain 64 slots per step, one slot
                         // per lane; matching lanes write consecutive positions.
+                        // Rows go lane by lane (a lane's rows own consecutive
+                        // positions, thread-major), so the wave's stores advance
+                        // through one region and every line is completed by the
+                        // next row's stores while it is still in L2 (slot by
+                        // slot, the wave kept 64 regions open, ~800 KB per CU,
+                        // and lines left L2 half written: REF-A join 3.3 ms).
                         const unsigned lane = threadIdx.x & 63u;
                         const u64 lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-#pragma unroll
-                        for (int i = 0; i < SI; ++i) {
+                        for (int l = 0; l < 64; ++l) {
                             if constexpr ((ABL & 2) != 0) break;
-                            const u64 key_i = R::key(sv_[i]);
-                            const u64 pay_i = (u64)R::pay(sv_[i]);
-                            const u64 pos_i = pos;
-                            pos += m[i];
-                            for (int l = 0; l < 64; ++l) {
+                            u64 p = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(pos >> 32), l) << 32) |
+                                    (u64)(unsigned)__builtin_amdgcn_readlane((int)pos, l);
+#pragma unroll
+                            for (int i = 0; i < SI; ++i) {
                                 if (__builtin_amdgcn_readlane((int)m[i], l) == 0) continue;   // uniform
+                                const u64 key_i = R::key(sv_[i]);
+                                const u64 pay_i = (u64)R::pay(sv_[i]);
                                 const u64 k = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(key_i >> 32), l) << 32) |
                                               (u64)(unsigned)__builtin_amdgcn_readlane((int)key_i, l);
                                 const PT sp_ = (PT)(((u64)(unsigned)__builtin_amdgcn_readlane((int)(pay_i >> 32), l) << 32) |
                                                     (u64)(unsigned)__builtin_amdgcn_readlane((int)pay_i, l));
-                                u64 p = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(pos_i >> 32), l) << 32) |
-                                        (u64)(unsigned)__builtin_amdgcn_readlane((int)pos_i, l);
                                 unsigned h = (unsigned)(rhash(k) >> a.tshift) & kMask;
                                 while (true) {
                                     const unsigned hs = (h + lane) & kMask;
