@@ -282,8 +282,8 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     HJ_TRY(ensure_buf(c->wstart, 1025 * 4));
     // work map: P + 1 chunk starts, then the item -> partition owner list
     const size_t items = (size_t)hj::radix_join_items(pl, fin.max_runs);
-    // work_start (P + 1) + work_owner (items) + deferred-item count and list (1 + items)
-    HJ_TRY(ensure_buf(c->work_start, (P + 2 + 2 * items) * 4));
+    // work_start (P + 1) + work_owner (items) + two deferred-item lists (1 + items each)
+    HJ_TRY(ensure_buf(c->work_start, (size_t)hj::radix_work_words(pl, fin.max_runs) * 4));
     HJ_TRY(ensure_buf(c->work_desc, items * hj::radix_item_desc_bytes()));
     HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
     return HJ_OK;

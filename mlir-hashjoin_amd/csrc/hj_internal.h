@@ -173,11 +173,14 @@ RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0
 RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set);
 unsigned long long radix_tiles(long long n, int max_nseg);
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs);
+// words of radix_join's work_start buffer: work map (P + 1 + items), then two
+// deferred-item lists (count + items each: the fast join's, the grouped join's)
+unsigned long long radix_work_words(const RadixPlan &pl, unsigned long long s_runs);
 // Partitioned rows are packed: 16 B {key, pay} (wide) or 8 B key << 32 | row id (narrow).
 hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
                            const BucketSet &out, hipStream_t st);
 size_t radix_item_desc_bytes();
-// work_start: >= P + 1 + radix_join_items words; desc: >= radix_join_items * radix_item_desc_bytes()
+// work_start: >= radix_work_words words; desc: >= radix_join_items * radix_item_desc_bytes()
 // join_stats (host-mapped, 2 words, may be null): the join leaves there
 // {items deferred by the fast path, items}; general = skip the fast path
 // (k_join over every item), chosen by the caller when the last join on the

@@ -817,9 +817,10 @@ struct ItemDesc {
 // (scalar) load instead of the owner -> partition -> offsets chain.
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
                                                    const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
-                                                   ItemDesc *desc, unsigned *zero) {
+                                                   ItemDesc *desc, unsigned *zero, unsigned *zero2) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
     if (w == 0 && zero) *zero = 0u;
+    if (w == 0 && zero2) *zero2 = 0u;
     if (w >= work_start[P]) return;
     const int p = (int)work_owner[w];
     const unsigned c = w - work_start[p];
@@ -1690,6 +1691,228 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     }
 }
 
+// --------------------------------------------------------------- grouped join
+// k_join_grp: narrow rows (the reference's i32 keys / row ids) whose build
+// keys repeat many times -- join-performances.md:3-6's 10M x 10M keys in
+// [1, 100k], ~100 copies of every key on both sides, ~1e9 pairs.  The
+// partition's build rows are GROUPED BY KEY in LDS instead of inserted into
+// a linear-probing table:
+//
+//   gkey[TS]   key << 32 | count, one slot per distinct key (open
+//              addressing, EMPTY = all ones: a count never reaches 2^32 - 1)
+//   gend[TS]   the key's group start, and after the placement its end
+//   grow[TS]   the build row ids, grouped by key
+//
+// build = one slot claim + one count add per row, a block scan of the
+// counts, one placement add per row; probe = one short walk per S row to its
+// key's (start, count); output = copies of the group, written lane-major
+// (each wave's stores advance through one output region).  The linear-
+// probing build walked every row past all earlier copies of its key (REF-A:
+// 0.65 ms of CAS walks) and the probe scanned the mixed cluster 64 slots per
+// step (profiles/r02_refa_join_ablation.txt).  Items of more than TS build
+// rows go to a.defer (k_join's rounds take them).  LIST: the items of a.list
+// (k_join_u's deferrals), with {items listed, items} into a.stats as k_join.
+template <bool WRITE, int NT, int RI, int SI, bool LIST>
+__global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
+    constexpr int TSL = 12, TS = 1 << TSL;
+    constexpr unsigned kMask = TS - 1;
+    constexpr int NW = NT / 64;
+    constexpr unsigned rb = (unsigned)(NW * RI), subb = (unsigned)(NW * SI);
+    constexpr unsigned rmax = (unsigned)TS >> kRunLog;   // runs: <= TS rows
+    constexpr int PER = TS / NT;                         // table slots per thread in the scan
+    static_assert(TS % NT == 0 && PER <= 16, "slots per thread");
+    constexpr u64 kE = ~0ull;
+    __shared__ u64 gkey[TS];
+    __shared__ unsigned gend[TS];
+    __shared__ unsigned grow[TS];
+    __shared__ u64 wsum[16];
+    __shared__ u64 s_base;
+    __shared__ unsigned s_rep;
+    const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
+    if (LIST && a.stats && blockIdx.x == 0 && threadIdx.x == 0) {
+        a.stats[0] = total;
+        a.stats[1] = a.work_start[a.P];
+    }
+    const u64 *rrows = (const u64 *)a.r;
+    const u64 *srows = (const u64 *)a.s;
+    unsigned *orr = (unsigned *)a.out_r;
+    unsigned *oss = (unsigned *)a.out_s;
+    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
+    const unsigned lane = threadIdx.x & 63u;
+    const u64 lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+    bool dup_sent = false;
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const u64 li = lo + (u64)i * NW + wv0;
+            e[i] = li < hi ? sload(list + li) : 0ull;
+        }
+    };
+    auto rows_of = [&](const u64 *rows, const u64 *e, u64 *v, int n) {
+        unsigned ok = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const bool in = lane < (unsigned)(e[i] & 127u);
+            v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + (in ? lane : 0u));
+            ok |= (unsigned)in << i;
+        }
+        return ok;
+    };
+    // slot of `key` (claimed when absent); the walk ends: <= TS keys per item
+    auto slot_of = [&](unsigned key) -> unsigned {
+        unsigned h = (unsigned)(rhash((u64)key) >> a.tshift) & kMask;
+        while (true) {
+            u64 e = gkey[h];
+            if (e == kE) {
+                e = atomicCAS(&gkey[h], kE, (u64)key << 32);
+                if (e == kE) return h;
+            }
+            if ((unsigned)(e >> 32) == key) return h;
+            h = (h + 1) & kMask;
+        }
+    };
+    for (unsigned w = blockIdx.x; w < total; w += gridDim.x) {
+        const unsigned wi = LIST ? a.list[w] : w;
+        const ItemDesc it = sload(a.desc + wi);
+        if (it.r_hi - it.r_lo > (u64)rmax) {   // uniform
+            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = wi;
+            continue;
+        }
+        for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)gkey)[j] = make_ulonglong2(kE, kE);
+        if (threadIdx.x == 0) s_rep = 0u;
+        __syncthreads();
+        // ---- count: every row claims / finds its key's slot and adds 1
+        const bool one_round = it.r_hi - it.r_lo <= (u64)rb;   // uniform: rows stay in registers
+        u64 rv[RI], er[RI];
+        unsigned rok = 0, rh[RI];
+        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
+            ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
+            rok = rows_of(rrows, er, rv, RI);
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                rh[i] = 0u;
+                if (!((rok >> i) & 1u)) continue;
+                rh[i] = slot_of((unsigned)(rv[i] >> 32));
+                atomicAdd(&gkey[rh[i]], 1ull);
+            }
+        }
+        __syncthreads();
+        // ---- group starts: exclusive scan of the counts in slot order
+        {
+            unsigned c[PER], sum = 0, rep = 0;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const u64 e = gkey[threadIdx.x * PER + j];
+                c[j] = e == kE ? 0u : (unsigned)e;
+                rep |= c[j] > 1u ? 1u : 0u;
+                sum += c[j];
+            }
+            u64 tot;
+            unsigned run = (unsigned)block_excl_scan<NT>((u64)sum, wsum, &tot);
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                gend[threadIdx.x * PER + j] = run;
+                run += c[j];
+            }
+            if (rep) s_rep = 1u;
+        }
+        __syncthreads();
+        if (s_rep && !dup_sent) {   // once per workgroup (k_join)
+            if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dup_sent = true;
+        }
+        // ---- placement: row ids into their key's group
+        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
+            if (!one_round) {
+                ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
+                rok = rows_of(rrows, er, rv, RI);
+            }
+#pragma unroll
+            for (int i = 0; i < RI; ++i) {
+                if (!((rok >> i) & 1u)) continue;
+                const unsigned h = one_round ? rh[i] : slot_of((unsigned)(rv[i] >> 32));
+                grow[atomicAdd(&gend[h], 1u)] = (unsigned)rv[i];
+            }
+        }
+        __syncthreads();
+        // ---- probe, one sub-chunk of S rows at a time
+        for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+            u64 es[SI], sv[SI];
+            ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
+            const unsigned sok = rows_of(srows, es, sv, SI);
+            unsigned cnt[SI], st[SI];
+            u64 mine = 0;
+#pragma unroll
+            for (int i = 0; i < SI; ++i) {
+                cnt[i] = st[i] = 0u;
+                if (!((sok >> i) & 1u)) continue;
+                const unsigned key = (unsigned)(sv[i] >> 32);
+                unsigned h = (unsigned)(rhash((u64)key) >> a.tshift) & kMask;
+                u64 e = gkey[h];
+                while (e != kE && (unsigned)(e >> 32) != key) {
+                    h = (h + 1) & kMask;
+                    e = gkey[h];
+                }
+                if (e != kE) {
+                    cnt[i] = (unsigned)e;
+                    st[i] = gend[h] - cnt[i];
+                }
+                mine += cnt[i];
+            }
+            u64 tot;
+            const u64 pre = block_excl_scan<NT>(mine, wsum, &tot);
+            if constexpr (!WRITE) {
+                if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                continue;
+            }
+            if (!tot) continue;   // uniform
+            if (threadIdx.x == 0) s_base = atomicAdd(a.counter, tot);
+            __syncthreads();
+            const u64 pos = s_base + pre;
+            if (tot > 2ull * (subb << kRunLog)) {
+                // many pairs per probe row: the wave copies one row's group at
+                // a time, 64 pairs per step, lane by lane (a lane's rows own
+                // consecutive positions, so the wave's stores stay in one region)
+                for (int l = 0; l < 64; ++l) {
+                    u64 p = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(pos >> 32), l) << 32) |
+                            (u64)(unsigned)__builtin_amdgcn_readlane((int)pos, l);
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)cnt[i], l);
+                        if (!c) continue;   // uniform
+                        const unsigned s0 = (unsigned)__builtin_amdgcn_readlane((int)st[i], l);
+                        const unsigned sp = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)sv[i], l);
+                        // (plain stores: a group's run starts and ends inside
+                        // lines, and non-temporal stores skip the L2 that
+                        // assembles them with the neighbouring rows' pairs)
+                        for (unsigned j = lane; j < c; j += 64u) {
+                            const u64 q = p + j;
+                            if (q < (u64)a.cap) {
+                                orr[q] = grow[s0 + j];
+                                oss[q] = sp;
+                            }
+                        }
+                        p += c;
+                    }
+                }
+            } else {
+                u64 q = pos;
+#pragma unroll
+                for (int i = 0; i < SI; ++i) {
+                    for (unsigned j = 0; j < cnt[i]; ++j, ++q) {
+                        if (q < (u64)a.cap) {
+                            orr[q] = grow[st[i] + j];
+                            oss[q] = (unsigned)sv[i];
+                        }
+                    }
+                }
+            }
+            __syncthreads();   // s_base reused by the next sub-chunk
+        }
+        __syncthreads();   // tables reused by the next item
+    }
+}
+
 // --------------------------------------------------------------- bucketized join
 // k_join2: the same work items as k_join, but the partition's LDS table is
 // BUCKETIZED and holds no keys:
@@ -2048,6 +2271,8 @@ constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 // (1024 threads x 4 S rows, 8 waves per SIMD): C2 join 9.45 -> 8.77 ms, C3
 // 2.79 -> 3.32 ms (profiles/r02_join_shapes.txt)
 constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
+// grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
+constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
 JoinVariant join_variant() {
     static int tsl = [] {
         const char *e = getenv("HJ_JOIN_TSL");
@@ -2160,6 +2385,10 @@ unsigned long long radix_tiles(long long n, int max_nseg) {
 }
 
 size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
+
+unsigned long long radix_work_words(const RadixPlan &pl, unsigned long long s_runs) {
+    return (1ull << pl.total_bits) + 3ull + 3ull * radix_join_items(pl, s_runs);
+}
 
 hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,
                               hipStream_t st) {
@@ -2295,11 +2524,15 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     if (want > chb) chb = (want + subb - 1) / subb * subb;
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
-    // fast path: the deferred-item list lives after the work map
+    // fast path: the deferred-item list lives after the work map; narrow rows
+    // (grp): repeated-key items go to k_join_grp, whose own deferrals
+    // (oversized partitions) follow in a second list for k_join
     unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
+    unsigned *defer2_n = defer_n + 1 + radix_join_items(pl, s_runs);
+    const bool grp = !wide && jv.kind == 0 && (fast || general);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc, fast ? defer_n : nullptr);
+                       (ItemDesc *)desc, fast ? defer_n : nullptr, grp ? defer2_n : nullptr);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -2342,6 +2575,8 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),      \
                                dim3(kFastNT), 0, st, a);                                                   \
     } while (0)
+#define HJ_JOINGRP(WR, LST) \
+    hipLaunchKernelGGL((k_join_grp<WR, kGrpNT, kGrpRI, kGrpSI, LST>), dim3(grid), dim3(kGrpNT), 0, st, a)
     if (fast) {
         a.defer = defer_n + 1;
         a.defer_n = defer_n;
@@ -2359,6 +2594,17 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         a.stats = join_stats;
 #define HJ_JOINL(W, WR) \
     hipLaunchKernelGGL((k_join<W, WR, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512), 0, st, a)
+        if (grp) {
+            // narrow rows: the grouped join takes the deferred items (its
+            // {listed, items} steer the next join), k_join what it defers
+            a.defer = defer2_n + 1;
+            a.defer_n = defer2_n;
+            if (count_only) HJ_JOINGRP(false, true);
+            else HJ_JOINGRP(true, true);
+            a.list = defer2_n + 1;
+            a.list_n = defer2_n;
+            a.stats = nullptr;
+        }
         if (wide) {
             if (count_only) HJ_JOINL(true, false);
             else HJ_JOINL(true, true);
@@ -2367,6 +2613,23 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             else HJ_JOINL(false, true);
         }
 #undef HJ_JOINL
+        return hipGetLastError();
+    }
+    if (grp) {
+        // narrow rows after a join that deferred most items (repeated keys):
+        // the grouped join over every item, k_join over what it defers; the
+        // steering stats stay those of the last fast join
+        a.defer = defer2_n + 1;
+        a.defer_n = defer2_n;
+        if (count_only) HJ_JOINGRP(false, false);
+        else HJ_JOINGRP(true, false);
+        a.list = defer2_n + 1;
+        a.list_n = defer2_n;
+        a.stats = nullptr;
+        if (count_only) hipLaunchKernelGGL((k_join<false, false, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid),
+                                           dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((k_join<false, true, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512),
+                                0, st, a);
         return hipGetLastError();
     }
     if (jv.kind == 3 || jv.kind == 4) {
@@ -2403,6 +2666,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         else HJ_JOIN_V(false, true);
     }
 #undef HJ_JOINP
+#undef HJ_JOINGRP
 #undef HJ_JOINU
 #undef HJ_JOIN2
 #undef HJ_JOIN_V

@@ -109,7 +109,7 @@ int main(int argc, char **argv) {
         printf("%s: runs %llu rows %llu partial runs %llu (%.2f/partition) max runs %llu max rows %llu\n",
                side ? "S" : "R", ps[P], rows, part, (double)part / P, maxr, maxrows);
     }
-    unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_runs));
+    unsigned *work = dalloc<unsigned>(radix_work_words(pl, ss.max_runs));
     void *desc = dalloc<char>(radix_join_items(pl, ss.max_runs) * radix_item_desc_bytes());
     u64 *out_r = dalloc<u64>(n + (1 << 20)), *out_s = dalloc<u64>(n + (1 << 20)), *cnt = dalloc<u64>(8),
         *dup = dalloc<u64>(8);

@@ -73,7 +73,7 @@ int main(int argc, char **argv) {
     CK(radix_partition(src, false, pl, ws, ss, 0));
     CK(hipDeviceSynchronize());
     const u64 cap = 1200000000ull;
-    unsigned *work = dalloc<unsigned>(P + 1 + radix_join_items(pl, ss.max_runs));
+    unsigned *work = dalloc<unsigned>(radix_work_words(pl, ss.max_runs));
     void *desc = dalloc<char>(radix_join_items(pl, ss.max_runs) * radix_item_desc_bytes());
     unsigned *out_r = dalloc<unsigned>(cap), *out_s = dalloc<unsigned>(cap);
     u64 *cnt = dalloc<u64>(8), *dup = dalloc<u64>(8);
@@ -104,6 +104,14 @@ int main(int argc, char **argv) {
     CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)cap, cnt, dup, false, 0,
                   stats, true, false));
     CK(hipDeviceSynchronize());
+    run("product general path (k_join_grp)", [&] {
+        CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)cap, cnt, dup, false, 0,
+                      stats, true, false));
+    });
+    run("product general, count only", [&] {
+        CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, 0, cnt, dup, true, 0, stats, true,
+                      false));
+    });
     JoinArgs a;
     a.r = rs.rows; a.s = ss.rows; a.r_runs = rs.runs; a.s_runs = ss.runs; a.r_rstart = rs.rstart;
     a.s_rstart = ss.rstart; a.P = P; a.work_start = work; a.desc = (const ItemDesc *)desc;
@@ -112,7 +120,7 @@ int main(int argc, char **argv) {
     const int cus = cu_count();
 #define J(WR, ABL, NAME) \
     run(NAME, [&] { hipLaunchKernelGGL((k_join<false, WR, 12, 512, ABL>), dim3(2 * cus), dim3(512), 0, 0, a); })
-    J(true, 0, "full");
+    J(true, 0, "k_join full");
     J(false, 0, "count only");
     J(true, 1, "no atomic");
     J(true, 2, "no writes");
