@@ -252,6 +252,40 @@ def test_radix_i32_many_matches_per_row(hj, oracle, bits):
     assert oracle.same_multiset(*o, exp[0].astype(np.int64), exp[1].astype(np.int64))
 
 
+def test_radix_i32_grouped_join_counts_capacity_and_repeats(oracle):
+    """Repeated i32 keys (~80 copies each, keys incl. -1 and INT32_MIN) on
+    one context, joined many times: the first join's fast path defers the
+    items to the grouped join (k_join_grp, list mode), the following ones run
+    it over every item; count-only calls, an output far smaller than M (the
+    count is still M, the rows written are true, distinct pairs) and a
+    resize-and-retry join must all agree with the oracle."""
+    r = oracle.gen_uniform_i32(81, 1, 1, 300, 24000)
+    s = oracle.gen_uniform_i32(81, 2, 1, 300, 18000)
+    r[:80] = -1; s[:5] = -1
+    r[80:160] = -(1 << 31); s[5:9] = -(1 << 31)
+    s[9:20] = 12345                   # no match
+    exp = oracle.chained_join_i32(r, s, H=300)
+    m = len(exp[0])
+    assert m > 50 * len(s)
+    h = HashJoin(0)
+    try:
+        h.set_strategy("radix", radix_bits=6)
+        for i in range(4):
+            h.build_table(dev(r), None)
+            assert h.count_rows(dev(s)) == m, f"count {i}"
+            out_r = torch.empty(1000, dtype=torch.int32, device="cuda"); out_s = torch.empty_like(out_r)
+            assert int(h.probe_relation(dev(s), None, out_r, out_s).item()) == m, f"probe {i}"
+            pr, ps = out_r.cpu().numpy().astype(np.int64), out_s.cpu().numpy().astype(np.int64)
+            assert (r[pr] == s[ps]).all() and len(set(zip(pr.tolist(), ps.tolist()))) == 1000, f"truncated {i}"
+            o_r, o_s = h.join(dev(r), None, dev(s), None, capacity=7)
+            torch.cuda.synchronize()
+            assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
+                                        exp[0].astype(np.int64), exp[1].astype(np.int64)), f"join {i}"
+        assert h.has_duplicates()
+    finally:
+        h.close()
+
+
 def test_fast_path_switch_repeated_joins(oracle):
     """Join-kernel choice across repeated joins on one context: a join whose
     items the fast path (k_join_u) mostly defers (i32 keys that repeat ~40x,
