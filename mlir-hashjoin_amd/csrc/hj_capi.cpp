@@ -157,10 +157,11 @@ struct hj_ctx {
     } memo;
     long long memo_hits = 0;
     // radix join kernel choice: the fast path (k_join_u) defers items it
-    // cannot take to k_join; the list-mode launch leaves {deferred, items}
-    // in join_stats (host-mapped).  When the last fast join deferred most of
-    // its items (keys that mostly repeat: the reference's 10M x 10M keys in
-    // [1, 100k]), the next joins skip the fast path, re-checking it every
+    // cannot take to k_join (narrow rows: to k_join_grp first); the list-mode
+    // launch leaves {deferred, items} in join_stats (host-mapped).  When the
+    // last fast join deferred most of its items (keys that mostly repeat: the
+    // reference's 10M x 10M keys in [1, 100k]), the next joins skip the fast
+    // path (narrow rows: k_join_grp over every item), re-checking it every
     // kFastRecheck joins.
     unsigned *join_stats = nullptr;       // host-mapped pinned, 2 words
     unsigned *join_stats_dev = nullptr;
