@@ -1709,8 +1709,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 // (each wave's stores advance through one output region).  The linear-
 // probing build walked every row past all earlier copies of its key (REF-A:
 // 0.65 ms of CAS walks) and the probe scanned the mixed cluster 64 slots per
-// step (profiles/r02_refa_join_ablation.txt).  Items of more than TS build
-// rows go to a.defer (k_join's rounds take them).  LIST: the items of a.list
+// step (profiles/r02_refa_join_ablation.txt).  Items of more than 63 runs
+// (> TS - 64 build rows) go to a.defer (k_join's rounds take them).  LIST: the items of a.list
 // (k_join_u's deferrals), with {items listed, items} into a.stats as k_join.
 template <bool WRITE, int NT, int RI, int SI, bool LIST>
 __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
@@ -1718,7 +1718,10 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     constexpr unsigned kMask = TS - 1;
     constexpr int NW = NT / 64;
     constexpr unsigned rb = (unsigned)(NW * RI), subb = (unsigned)(NW * SI);
-    constexpr unsigned rmax = (unsigned)TS >> kRunLog;   // runs: <= TS rows
+    // runs: <= TS - 64 rows, so >= 64 slots stay EMPTY and every walk ends
+    // (64 full runs of distinct keys would fill the table, and a probe for a
+    // missing key would never meet EMPTY)
+    constexpr unsigned rmax = ((unsigned)TS >> kRunLog) - 1u;
     constexpr int PER = TS / NT;                         // table slots per thread in the scan
     static_assert(TS % NT == 0 && PER <= 16, "slots per thread");
     constexpr u64 kE = ~0ull;

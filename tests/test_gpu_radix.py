@@ -282,6 +282,17 @@ def test_radix_i32_grouped_join_counts_capacity_and_repeats(oracle):
             assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
                                         exp[0].astype(np.int64), exp[1].astype(np.int64)), f"join {i}"
         assert h.has_duplicates()
+        # the context now runs the grouped join on every narrow item: distinct
+        # keys at ~4000 build rows per partition (near-full 4096-slot tables,
+        # the largest items deferred on to k_join) and probes that miss
+        ru = np.random.default_rng(5).permutation(1 << 20)[:64000].astype(np.int32) * 3 + 1
+        su = np.concatenate([ru[::2], ru[1::7] + 1]).astype(np.int32)
+        h.set_strategy("radix", radix_bits=4)
+        o_r, o_s = h.join(dev(ru), None, dev(su), None)
+        torch.cuda.synchronize()
+        ex = oracle.chained_join_i32(ru, su, H=1000)
+        assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
+                                    ex[0].astype(np.int64), ex[1].astype(np.int64))
     finally:
         h.close()
 
