@@ -329,7 +329,7 @@ def main():
 
         def step(acc):
             ev = {}
-            o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev)
+            o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev, n_build_global=NR)
             ev["probed"].synchronize()
             if acc:
                 # transfers overlap compute (hashjoin.dist): R's tuples move

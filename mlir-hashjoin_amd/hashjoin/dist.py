@@ -168,7 +168,7 @@ def _probe_all(hj, tuples, capacity):
 
 
 def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None,
-                     replicate_max_rows=None, max_rows=None, self_p2p=False):
+                     replicate_max_rows=None, max_rows=None, self_p2p=False, n_build_global=None):
     """Join this rank's slices of R and S against every other rank's.
 
     hj: a hashjoin.HashJoin on this rank's GPU (or any object with its
@@ -177,17 +177,22 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     owns (shuffle) or of its own S rows (replicate).  `phases`, if a dict,
     receives events (start, routed, built, probed) for timing (CUDA events on
     GPU tensors, else host timestamps), "rows" = (R rows built, S rows
-    probed) and "mode" = "shuffle" | "replicate"."""
+    probed) and "mode" = "shuffle" | "replicate".  n_build_global: |R| over
+    all ranks when the caller knows it (the same value on every rank); it
+    saves the all-reduce and host round trip that otherwise decide between
+    replicating and shuffling R (~0.15 ms per call)."""
     if replicate_max_rows is None:
         replicate_max_rows = REPLICATE_MAX_ROWS
     cuda = rkey.is_cuda
     ev = (lambda name: _event(phases, name, cuda)) if phases is not None else (lambda name: None)
     ev("start")
-    n_r = torch.tensor([rkey.numel()], dtype=torch.int64, device=rkey.device)
-    dist.all_reduce(n_r, group=group)
-    if int(n_r.item()) <= replicate_max_rows:
+    if n_build_global is None:
+        n_r = torch.tensor([rkey.numel()], dtype=torch.int64, device=rkey.device)
+        dist.all_reduce(n_r, group=group)
+        n_build_global = int(n_r.item())
+    if int(n_build_global) <= replicate_max_rows:
         # small build side: every rank builds all of R, S stays where it is
-        _dbg("replicate", int(n_r.item()), skey.numel())
+        _dbg("replicate", int(n_build_global), skey.numel())
         mine = torch.stack([rkey, rpay], dim=1).contiguous()
         all_r = all_gather_rows(mine, group)
         local_s = torch.stack([skey, spay], dim=1).contiguous()

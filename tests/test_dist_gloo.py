@@ -155,7 +155,8 @@ def _dj_worker(rank, world, port, case, outdir):
     hj = _CpuJoin()
     ph = {}
     o_r, o_s = distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
-                                replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"))
+                                replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"),
+                                n_build_global=case["NR"] if case.get("known_nr") else None)
     nrows = ph["rows"]
     if ph["mode"] == "shuffle":
         # every output key is owned here (S.pay of the generators is the global row id)
@@ -181,8 +182,10 @@ def _dj_worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=700, NS=9000, frac=1.0, seed=26, replicate=1 << 21),  # small R: replicated
     dict(dist="uniform", NR=900, NS=1200, hi=50, seed=27, replicate=1 << 21, world=3, capacity=5),
     dict(dist="pkfk", NR=5, NS=3, frac=1.0, seed=28, world=4),                 # ranks without rows
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=29, known_nr=True),     # |R| given: no all-reduce
+    dict(dist="pkfk", NR=700, NS=9000, frac=1.0, seed=30, replicate=1 << 21, known_nr=True, world=3),
 ], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
-        "tiny_4ranks"])
+        "tiny_4ranks", "known_build_size", "known_build_size_replicate"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
