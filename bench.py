@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--radix-bits", type=int, default=0)
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU code path (partition + all-to-all) even at N=1")
+    ap.add_argument("--s-parts", type=int, default=0,
+                    help="multi-GPU path: batches the shuffled probe side moves in (0: hashjoin.dist default)")
     ap.add_argument("--log2", type=int, default=0,
                     help="experiments: |R| = |S| = 2^LOG2 rows instead of the config's sizes (not a bench line)")
     return ap.parse_args()
@@ -329,7 +331,8 @@ def main():
 
         def step(acc):
             ev = {}
-            o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev, n_build_global=NR)
+            o_r, o_s = distributed_join(hj, rk, rp, sk, sp, phases=ev, n_build_global=NR,
+                                        s_parts=a.s_parts or None)
             ev["probed"].synchronize()
             if acc:
                 # transfers overlap compute (hashjoin.dist): R's tuples move

@@ -57,17 +57,19 @@ def _dbg(*a):
 MAX_ROWS_PER_ROUND = 1 << 26
 
 
-def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows, self_p2p=False):
+def _all_to_all_rows(recv, send, out_rows, in_rows, group, max_rows, self_p2p=False, in_off=None):
     """recv[rows from p] <- every p's send[rows for me]: one batched group of
     point-to-point messages of at most max_rows rows each (views, no staging
     copies).  Sender and receiver cut a slice into the same pieces because
     in_rows on p and out_rows here describe the same slice.  The slice a rank
     keeps is copied locally unless self_p2p (tests: it then goes through the
-    backend like any other slice, cut into the same pieces).  Returns the
-    outstanding works (wait on them before reading recv)."""
+    backend like any other slice, cut into the same pieces).  in_off: where
+    each destination's rows start in send (default: packed in rank order).
+    Returns the outstanding works (wait on them before reading recv)."""
     world = len(in_rows)
     me = dist.get_rank(group)
-    in_off = [sum(in_rows[:p]) for p in range(world)]
+    if in_off is None:
+        in_off = [sum(in_rows[:p]) for p in range(world)]
     out_off = [sum(out_rows[:p]) for p in range(world)]
     ops = []
     if self_p2p:
@@ -96,15 +98,24 @@ class Exchange:
     """One routed tuple buffer in flight: counts are exchanged at start
     (blocking: they size the receive buffer), the tuples move asynchronously
     (batched point-to-point on the backend's stream).  `wait()` orders the
-    current stream after the transfer; `recv` is valid from then on."""
+    current stream after the transfer; `recv` is valid from then on.
 
-    def __init__(self, send, counts, group=None, max_rows=None, self_p2p=False):
+    parts > 1: every rank's slice moves as `parts` consecutive batches (part
+    k = rows [n k / parts, n (k + 1) / parts) of each slice, the same cut on
+    both ends), and recv holds part 0's rows from every rank, then part 1's,
+    ...: `wait_part(k)` returns part k as soon as it has arrived, so the
+    caller can work on it while the later parts are still on the links."""
+
+    def __init__(self, send, counts, group=None, max_rows=None, self_p2p=False, parts=1):
         world = dist.get_world_size(group)
         if counts.numel() != world:
             raise ValueError("one count per rank required")
         max_rows = MAX_ROWS_PER_ROUND if max_rows is None else int(max_rows)
         if max_rows < 1:
             raise ValueError("max_rows must be positive")
+        parts = int(parts)
+        if parts < 1:
+            raise ValueError("parts must be positive")
         counts = counts.contiguous()
         recv_counts = torch.empty_like(counts)
         dist.all_to_all_single(recv_counts, counts, group=group)
@@ -112,12 +123,32 @@ class Exchange:
         self.in_rows, self.out_rows = host[0].tolist(), host[1].tolist()
         self.send = send   # kept alive until the transfer is done
         self.recv = torch.empty((sum(self.out_rows), 2), dtype=torch.int64, device=send.device)
-        self._works = _all_to_all_rows(self.recv, send, self.out_rows, self.in_rows, group, max_rows, self_p2p)
+        in_off = [sum(self.in_rows[:p]) for p in range(world)]
+        cut = lambda n, k: n * k // parts  # noqa: E731
+        self._parts = []
+        base = 0
+        for k in range(parts):
+            in_k = [cut(n, k + 1) - cut(n, k) for n in self.in_rows]
+            out_k = [cut(n, k + 1) - cut(n, k) for n in self.out_rows]
+            off_k = [in_off[p] + cut(self.in_rows[p], k) for p in range(world)]
+            recv_k = self.recv[base:base + sum(out_k)]
+            base += sum(out_k)
+            works = _all_to_all_rows(recv_k, send, out_k, in_k, group, max_rows, self_p2p, in_off=off_k)
+            self._parts.append([recv_k, works])
+
+    @property
+    def parts(self):
+        return len(self._parts)
+
+    def wait_part(self, k):
+        for w in self._parts[k][1]:
+            w.wait()
+        self._parts[k][1] = []
+        return self._parts[k][0]
 
     def wait(self):
-        for w in self._works:
-            w.wait()
-        self._works = []
+        for k in range(len(self._parts)):
+            self.wait_part(k)
         return self.recv
 
 
@@ -167,8 +198,41 @@ def _probe_all(hj, tuples, capacity):
     raise RuntimeError("distributed join output did not fit after resizing")
 
 
+def _probe_parts(hj, parts, capacity, total, device):
+    """Probe each received part of S as soon as it is there (callables that
+    wait for it), into one output sized `capacity` (default: the S rows
+    received); a part whose pairs do not fit what is left is probed again
+    into a buffer of its own at the exact M and the pieces are joined."""
+    cap = max(1, total if capacity is None else int(capacity))
+    out_r = torch.empty(cap, dtype=torch.int64, device=device)
+    out_s = torch.empty(cap, dtype=torch.int64, device=device)
+    pos, extra = 0, []
+    for get in parts:
+        t = get()
+        if t.shape[0] == 0:
+            continue
+        m = None
+        if cap > pos:
+            m = int(hj.probe_tuples(t, out_r[pos:], out_s[pos:]).item())
+            if m <= cap - pos:
+                pos += m
+                continue
+        extra.append(_probe_all(hj, t, m))   # (the rows written past pos are dropped)
+    if not extra:
+        return out_r[:pos], out_s[:pos]
+    return (torch.cat([out_r[:pos]] + [e[0] for e in extra]), torch.cat([out_s[:pos]] + [e[1] for e in extra]))
+
+
+# S moves in this many consecutive batches when ranks exchange over links, so
+# that the probe of one part overlaps the transfer of the next (a part of
+# 2^24 rows probes in ~0.56 ms, about what its 0.25 GiB take on the links at
+# N = 8); at world size 1 there is no transfer to hide.
+S_PARTS = 2
+
+
 def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None,
-                     replicate_max_rows=None, max_rows=None, self_p2p=False, n_build_global=None):
+                     replicate_max_rows=None, max_rows=None, self_p2p=False, n_build_global=None,
+                     s_parts=None):
     """Join this rank's slices of R and S against every other rank's.
 
     hj: a hashjoin.HashJoin on this rank's GPU (or any object with its
@@ -180,7 +244,8 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     probed) and "mode" = "shuffle" | "replicate".  n_build_global: |R| over
     all ranks when the caller knows it (the same value on every rank); it
     saves the all-reduce and host round trip that otherwise decide between
-    replicating and shuffling R (~0.15 ms per call)."""
+    replicating and shuffling R (~0.15 ms per call).  s_parts: batches the
+    shuffled S moves in (default S_PARTS, 1 at world size 1)."""
     if replicate_max_rows is None:
         replicate_max_rows = REPLICATE_MAX_ROWS
     cuda = rkey.is_cuda
@@ -208,19 +273,22 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     _dbg("route", rkey.numel(), skey.numel())
     send_r, cr = hj.partition(rkey, rpay, dist.get_world_size(group))
     xr = Exchange(send_r, cr, group, max_rows, self_p2p)
-    send_s, cs = hj.partition(skey, spay, dist.get_world_size(group))
-    xs = Exchange(send_s, cs, group, max_rows, self_p2p)
+    world = dist.get_world_size(group)
+    send_s, cs = hj.partition(skey, spay, world)
+    if s_parts is None:
+        s_parts = S_PARTS if world > 1 else 1
+    xs = Exchange(send_s, cs, group, max_rows, self_p2p, parts=s_parts)
     ev("routed")
     recv_r = xr.wait()
     _dbg("build", recv_r.shape[0])
     hj.build_tuples(recv_r)
     ev("built")
-    recv_s = xs.wait()
-    _dbg("probe", recv_s.shape[0])
+    n_s = sum(xs.out_rows)
+    _dbg("probe", n_s, xs.parts)
     if phases is not None:
-        phases["rows"] = (recv_r.shape[0], recv_s.shape[0])
+        phases["rows"] = (recv_r.shape[0], n_s)
         phases["mode"] = "shuffle"
-    out = _probe_all(hj, recv_s, capacity)
+    out = _probe_parts(hj, [lambda k=k: xs.wait_part(k) for k in range(xs.parts)], capacity, n_s, rkey.device)
     ev("probed")
     return out
 

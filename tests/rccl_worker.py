@@ -44,7 +44,9 @@ def main():
         for mode, kw in (("shuffle", dict(replicate_max_rows=0, max_rows=4093, self_p2p=True)),
                          ("shuffle_copy", dict(replicate_max_rows=0)),
                          ("replicate", dict(replicate_max_rows=1 << 21)),
-                         ("resize", dict(replicate_max_rows=0, capacity=3, self_p2p=True))):
+                         ("resize", dict(replicate_max_rows=0, capacity=3, self_p2p=True)),
+                         ("s_parts", dict(replicate_max_rows=0, max_rows=2999, self_p2p=True, s_parts=3)),
+                         ("s_parts_overflow", dict(replicate_max_rows=0, self_p2p=True, s_parts=2, capacity=2000))):
             ph = {}
             o_r, o_s = distributed_join(hj, d(rk), d(rp), d(sk), d(sp), phases=ph, **kw)
             torch.cuda.synchronize()

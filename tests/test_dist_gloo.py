@@ -156,7 +156,8 @@ def _dj_worker(rank, world, port, case, outdir):
     ph = {}
     o_r, o_s = distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
                                 replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"),
-                                n_build_global=case["NR"] if case.get("known_nr") else None)
+                                n_build_global=case["NR"] if case.get("known_nr") else None,
+                                s_parts=case.get("s_parts"))
     nrows = ph["rows"]
     if ph["mode"] == "shuffle":
         # every output key is owned here (S.pay of the generators is the global row id)
@@ -184,8 +185,12 @@ def _dj_worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=5, NS=3, frac=1.0, seed=28, world=4),                 # ranks without rows
     dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=29, known_nr=True),     # |R| given: no all-reduce
     dict(dist="pkfk", NR=700, NS=9000, frac=1.0, seed=30, replicate=1 << 21, known_nr=True, world=3),
+    dict(dist="pkfk", NR=3000, NS=5001, frac=0.9, seed=31, s_parts=3, world=3, max_rows=113),  # S in 3 batches
+    dict(dist="uniform", NR=2000, NS=2500, hi=200, seed=32, s_parts=4, capacity=1000),  # parts overflow the output
+    dict(dist="pkfk", NR=7, NS=2, frac=1.0, seed=33, s_parts=5, world=2),               # empty parts
 ], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
-        "tiny_4ranks", "known_build_size", "known_build_size_replicate"])
+        "tiny_4ranks", "known_build_size", "known_build_size_replicate", "s_parts3", "s_parts_overflow",
+        "s_parts_empty"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
