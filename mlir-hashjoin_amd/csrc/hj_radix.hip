@@ -723,15 +723,28 @@ __global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const uns
     if (lds)
         for (int i = threadIdx.x; i < P; i += 1024) cr[i] = 0u;
     __syncthreads();
+    const unsigned lane = threadIdx.x & 63u;
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
         const unsigned b = j < n ? bbin[j] : kNoBucket;
-        if (b < (unsigned)P) {
-            const unsigned nr = runs_of(bfill[j]);
-            if (lds) atomicAdd(&cr[b], nr);
-            else atomicAdd(&rcnt[b], (u64)nr);
+        const bool valid = b < (unsigned)P;
+        const unsigned nr = valid ? runs_of(bfill[j]) : 0u;
+        if (lds) {
+            if (valid) atomicAdd(&cr[b], nr);
+            continue;
         }
+        // the wave's lanes that hold the same partition as its first valid
+        // lane add once (a skewed key's buckets are consecutive ids: C4's hot
+        // partition put ~10^4 same-address atomics on one counter, 0.11 ms)
+        const u64 vm = __ballot(valid);
+        if (!vm) continue;   // uniform
+        const int l0 = __ffsll((long long)vm) - 1;
+        const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)b, l0);
+        const bool same = valid && b == b0;
+        const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)wave_incl_add(same ? nr : 0u), 63);
+        if (valid && !same) atomicAdd(&rcnt[b], (u64)nr);
+        if ((int)lane == l0) atomicAdd(&rcnt[b0], (u64)tot);
     }
     if (!lds) return;
     __syncthreads();
@@ -755,14 +768,43 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
         }
     };
     if (P > kListLds) {
+        // as k_bcount: the lanes of the wave's first partition take their
+        // places from one cursor add (prefix of their run counts), the
+        // others one add each; all adds issue before any result is used
+        const unsigned lane = threadIdx.x & 63u;
+        unsigned bi[kListPer], fi[kListPer], pre[kListPer], l0i[kListPer];
+        u64 ri[kListPer];
 #pragma unroll
         for (int i = 0; i < kListPer; ++i) {
             const u64 j = base + (u64)i * 1024 + threadIdx.x;
-            const unsigned b = j < n ? bbin[j] : kNoBucket;
-            if (b < (unsigned)P) {
-                const unsigned f = bfill[j];
-                put_runs(j, f, rstart[b] + atomicAdd(&rcur[b], (u64)runs_of(f)));
-            }
+            bi[i] = j < n ? bbin[j] : kNoBucket;
+            const bool valid = bi[i] < (unsigned)P;
+            fi[i] = valid ? bfill[j] : 0u;
+            const unsigned nr = runs_of(fi[i]);
+            const u64 vm = __ballot(valid);
+            l0i[i] = vm ? (unsigned)__ffsll((long long)vm) - 1u : 64u;   // uniform
+            ri[i] = 0ull;
+            pre[i] = 0u;
+            if (!vm) continue;
+            const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bi[i], (int)l0i[i]);
+            const bool same = valid && bi[i] == b0;
+            const unsigned v = same ? nr : 0u;
+            const unsigned incl = wave_incl_add(v);
+            const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)incl, 63);
+            pre[i] = same ? incl - v : ~0u;   // ~0: not in the group
+            if (valid && !same) ri[i] = atomicAdd(&rcur[bi[i]], (u64)nr);
+            if (lane == l0i[i]) ri[i] = atomicAdd(&rcur[b0], (u64)tot);
+        }
+#pragma unroll
+        for (int i = 0; i < kListPer; ++i) {
+            if (l0i[i] == 64u) continue;   // uniform: no valid lane
+            const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bi[i], (int)l0i[i]);
+            const u64 g = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(ri[i] >> 32), (int)l0i[i]) << 32) |
+                          (u64)(unsigned)__builtin_amdgcn_readlane((int)ri[i], (int)l0i[i]);
+            if (bi[i] >= (unsigned)P) continue;
+            const u64 j = base + (u64)i * 1024 + threadIdx.x;
+            const u64 at = pre[i] != ~0u ? rstart[b0] + g + pre[i] : rstart[bi[i]] + ri[i];
+            put_runs(j, fi[i], at);
         }
         return;
     }
