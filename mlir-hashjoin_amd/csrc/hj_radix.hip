@@ -1414,7 +1414,14 @@ __device__ __forceinline__ ItemDesc sload(const ItemDesc *p) {
     return ItemDesc{sload(q), sload(q + 1), sload(q + 2), sload(q + 3)};
 }
 
-template <bool WIDE, bool WRITE, int TSL, int NT, int RI, int SI, int WPS, bool GEN = true>
+// ABL (micro/join3_micro.hip ablations only; 0 in the product): bit 0 no
+// output cursor atomic (a per-item position instead), bit 1 no output
+// stores, bit 2 no probe walks, bit 3 no build inserts, bit 4 no build
+// collision walks, bit 5 no payload stores into the table (an interleaved
+// form of the collision walks, every row's CAS in flight at once, measured
+// slower: C3 join 2.75 -> 2.99 ms; so was a walk reading the aligned slot
+// pair ahead and CASing only an EMPTY slot: narrow 1.85 -> 2.25 ms)
+template <bool WIDE, bool WRITE, int TSL, int NT, int RI, int SI, int WPS, bool GEN = true, int ABL = 0>
 __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -1511,7 +1518,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
                 const u64 key = R::key(rv_[i]);
-                bool act = (rok >> i) & 1u;
+                bool act = ((rok >> i) & 1u) && !(ABL & 8);
                 if (WIDE && act && key == kEmptyKey64) {   // the null pass lives in k_join
                     bad = true;
                     act = false;
@@ -1536,13 +1543,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                 unsigned h = hb[i];
                 u64 old = ob[i];
                 bool d = false;
-                while (old != kEmpty) {
+                while (!(ABL & 16) && old != kEmpty) {
                     d |= WIDE ? (old == key) : ((old >> 32) == key);
                     h = (h + 1) & kMask;
                     old = atomicCAS(&tkey[h], kEmpty, vb[i]);
                 }
                 ndup += d ? 1u : 0u;
-                if constexpr (WIDE) tpay[h] = R::pay(rv_[i]);
+                if constexpr (WIDE && !(ABL & 32)) tpay[h] = R::pay(rv_[i]);
             }
             r0 += rb;
             if (r0 >= it.r_hi) break;
@@ -1577,7 +1584,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                     unsigned pm = 0u;   // bit i: row slot i probes
 #pragma unroll
                     for (int i = 0; i < SI; ++i)
-                        if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64)) pm |= 1u << i;
+                        if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64) && !(ABL & 4)) pm |= 1u << i;
                     if (GEN && !unique) {
                         // a repeated build key: every row walks its chain to
                         // EMPTY, counting, then again writing at its prefix
@@ -1697,11 +1704,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
                             run += v[k];
                         }
                         if (lane == 63 && x) {
-                            if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
+                            if constexpr (ABL & 1) s_base = ((u64)w << 11) % (u64)(a.cap > 8192 ? a.cap - 8192 : 1);
+                            else if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
                             else atomicAdd(a.counter, (u64)x);
                         }
                     }
-                    if constexpr (WRITE) {
+                    if constexpr (WRITE && !(ABL & 2)) {
                         __syncthreads();
 #pragma unroll
                         for (int i = 0; i < SI; ++i) {
