@@ -582,21 +582,33 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P,
 // writes each row to its own rank slot (lanes of a wave hit unrelated
 // addresses and most 128-B lines are written in pieces, each a
 // read-modify-write in HBM: profiles/r01_micro_write_alignment.txt).
+// Two shapes: up to 512 parts, 8192-row tiles (152 KiB of LDS: one
+// workgroup per CU, whose load and store phases then alternate on the CU);
+// 4..64 parts (the multi-GPU owner routing: one part per rank), 2048-row
+// tiles in 37 KiB, four workgroups per CU overlapping each other's phases:
+// 8 parts 4.22 -> 2.78 ms and 64 parts 6.11 -> 3.33 ms per 2^28 rows
+// (profiles/r02_route_tiles.txt).  1-2 parts keep the large tile (2-5 %
+// faster there); a 128-part small tile (38 KiB) and a 4096-row tile for
+// 65..256 parts measured no better than the large one.
 constexpr int kRouteTile = 8192;
 constexpr int kRouteThreads = 1024;
 constexpr int kRouteMaxParts = 512;
+constexpr int kRouteTileS = 2048;
+constexpr int kRouteThreadsS = 256;
+constexpr int kRouteMaxPartsS = 64;
 
-template <int FORM>
-__global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, unsigned P, ulonglong2 *out,
-                                                                 unsigned long long *cursors) {
-    constexpr int IT = kRouteTile / kRouteThreads;
-    __shared__ ulonglong2 stage[kRouteTile];
-    __shared__ unsigned short sp[kRouteTile];
-    __shared__ unsigned cnt[kRouteMaxParts], start[kRouteMaxParts];
-    __shared__ unsigned long long base[kRouteMaxParts];
-    for (unsigned i = threadIdx.x; i < P; i += kRouteThreads) cnt[i] = 0u;
+template <int FORM, int TILE, int NT, int MAXP>
+__global__ __launch_bounds__(NT) void k_route_scatter(SrcDev src, unsigned P, ulonglong2 *out,
+                                                      unsigned long long *cursors) {
+    constexpr int IT = TILE / NT;
+    static_assert(MAXP % 64 == 0 && TILE % NT == 0 && IT % 2 == 0, "route tile shape");
+    __shared__ ulonglong2 stage[TILE];
+    __shared__ unsigned short sp[TILE];
+    __shared__ unsigned cnt[MAXP], start[MAXP];
+    __shared__ unsigned long long base[MAXP];
+    for (unsigned i = threadIdx.x; i < P; i += NT) cnt[i] = 0u;
     __syncthreads();
-    const long long lo = (long long)blockIdx.x * kRouteTile;
+    const long long lo = (long long)blockIdx.x * TILE;
     ulonglong2 row[IT];
     unsigned pr[IT];   // part << 16 | rank, or ~0
     if constexpr (FORM == kCols64) {
@@ -605,7 +617,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, uns
         const bool al = ((((uintptr_t)kc) | ((uintptr_t)pc)) & 15) == 0;
 #pragma unroll
         for (int i = 0; i < IT / 2; ++i) {
-            const long long r = lo + 2ll * (i * kRouteThreads + threadIdx.x);
+            const long long r = lo + 2ll * (i * NT + threadIdx.x);
             if (al && r + 1 < src.n) {
                 const ulonglong2 k2 = *(const ulonglong2 *)(kc + r), p2 = *(const ulonglong2 *)(pc + r);
                 row[2 * i] = make_ulonglong2(k2.x, p2.x);
@@ -622,7 +634,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, uns
     } else {
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const long long r = lo + (long long)i * kRouteThreads + threadIdx.x;
+            const long long r = lo + (long long)i * NT + threadIdx.x;
             const bool v = r < src.n;
             const Tuple tp = v ? load_src<FORM>(src, r) : Tuple{0ull, 0ull};
             row[i] = make_ulonglong2(tp.k, tp.p);
@@ -643,7 +655,7 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, uns
     __syncthreads();
     if (threadIdx.x < 64) {   // wave 0: stage offsets; one cursor atomic per non-empty part
         const unsigned lane = threadIdx.x;
-        constexpr int PER = kRouteMaxParts / 64;
+        constexpr int PER = MAXP / 64;
         unsigned c[PER], sum = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
@@ -678,10 +690,10 @@ __global__ __launch_bounds__(kRouteThreads) void k_route_scatter(SrcDev src, uns
     }
     __syncthreads();
     const long long rem = src.n - lo;
-    const unsigned tn = rem < kRouteTile ? (unsigned)rem : (unsigned)kRouteTile;
+    const unsigned tn = rem < TILE ? (unsigned)rem : (unsigned)TILE;
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-        const unsigned j = (unsigned)i * kRouteThreads + threadIdx.x;
+        const unsigned j = (unsigned)i * NT + threadIdx.x;
         if (j >= tn) continue;
         const unsigned d = sp[j];
         out[base[d] + (j - start[d])] = stage[j];
@@ -1014,14 +1026,22 @@ hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
         else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, counts);
         else return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(64), 0, st, counts, P, cursors);
-        if (P <= (unsigned)kRouteMaxParts) {
+        if (P >= 4u && P <= (unsigned)kRouteMaxPartsS) {
+            const unsigned gt = grid_for(src.n, kRouteTileS);
+            if (src.form == kCols64)
+                hipLaunchKernelGGL((k_route_scatter<kCols64, kRouteTileS, kRouteThreadsS, kRouteMaxPartsS>), dim3(gt),
+                                   dim3(kRouteThreadsS), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+            else
+                hipLaunchKernelGGL((k_route_scatter<kPacked64, kRouteTileS, kRouteThreadsS, kRouteMaxPartsS>), dim3(gt),
+                                   dim3(kRouteThreadsS), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+        } else if (P <= (unsigned)kRouteMaxParts) {
             const unsigned gt = grid_for(src.n, kRouteTile);
             if (src.form == kCols64)
-                hipLaunchKernelGGL(k_route_scatter<kCols64>, dim3(gt), dim3(kRouteThreads), 0, st, src, P,
-                                   (ulonglong2 *)out_tuples, cursors);
+                hipLaunchKernelGGL((k_route_scatter<kCols64, kRouteTile, kRouteThreads, kRouteMaxParts>), dim3(gt),
+                                   dim3(kRouteThreads), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
             else
-                hipLaunchKernelGGL(k_route_scatter<kPacked64>, dim3(gt), dim3(kRouteThreads), 0, st, src, P,
-                                   (ulonglong2 *)out_tuples, cursors);
+                hipLaunchKernelGGL((k_route_scatter<kPacked64, kRouteTile, kRouteThreads, kRouteMaxParts>), dim3(gt),
+                                   dim3(kRouteThreads), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
         } else if (src.form == kCols64)
             hipLaunchKernelGGL(k_part_scatter<kCols64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
         else
