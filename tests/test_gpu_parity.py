@@ -283,7 +283,7 @@ def test_partition_fanout_limit(hj):
         hj.partition(k, k, 8193)
 
 
-@pytest.mark.parametrize("P", [1, 2, 3, 8, 257, 1000, 4096, 8192])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8, 64, 65, 257, 1000, 4096, 8192])
 def test_partition_kernel(hj, oracle, P):
     from test_abi import _np_partition_of
     k, p = oracle.gen_uniform_i64(P, 1, -(1 << 62), 1 << 62, 12345)
@@ -301,6 +301,23 @@ def test_partition_kernel(hj, oracle, P):
     # packed-tuple input form routes identically
     out2, counts2 = hj.partition(torch.from_numpy(out).cuda(), None, P)
     assert np.array_equal(host(counts2), counts)
+
+
+@pytest.mark.parametrize("P,n", [(8, 2048 * 5 + 77), (64, 2048 * 3), (4, 1), (6, 0)])
+def test_partition_skewed_and_ragged(hj, oracle, P, n):
+    """The 2048-row route tiles (4..64 parts): one hot key taking 3/4 of the
+    rows, ragged and empty inputs; counts, owners and the multiset exact."""
+    from test_abi import _np_partition_of
+    k, p = oracle.gen_uniform_i64(P + 100, 2, -(1 << 62), 1 << 62, n)
+    k[: (3 * n) // 4] = 12345
+    out, counts = hj.partition(dev(k), dev(p), P)
+    torch.cuda.synchronize()
+    out = host(out); counts = host(counts)
+    assert np.array_equal(counts, np.bincount(_np_partition_of(k, P), minlength=P))
+    off = np.concatenate([[0], np.cumsum(counts)])
+    for q in range(P):
+        assert (_np_partition_of(out[off[q]:off[q + 1], 0], P) == q).all()
+    assert oracle.same_multiset(out[:, 0], out[:, 1], k, p)
 
 
 def test_tuple_build_probe(hj, oracle):
