@@ -15,7 +15,8 @@ join of the whole relations with inputs resident in HBM:
 value = |S| / (time per step), the whole job over all ranks (max over ranks).
 `roofline` is SURVEY 8(d)'s probe-phase figure: 48 B per probe tuple (16 B S
 row + 16 B slot + 16 B output pair) over the probe phase's HIP-event time;
-`roofline.kernel` is the same for the dominant kernel (k_join_u) alone.
+`roofline.kernel` is the same for the dominant kernel (the LDS join: k_join_b
+for int64 rows, k_join_u for i32 rows and probe-heavy joins) alone.
 Launch:  python bench.py [--gpus 1 --steps K --warmup W --config C3]
          python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
@@ -56,10 +57,12 @@ REFERENCE_PUBLISHED = {
     "REF-A": {"join_v1_s": 2.0, "join_v2_s": 1.5, "source": "join-performances.md:3-6, :16-19"},
     "REF-B": {"join_v1_s": 12.0, "join_v2_s": 12.5, "source": "join-performances.md:8-11, :21-24"},
 }
-# probe phase: S partition passes + the LDS join (k_join_u; k_join takes the
-# items k_join_u defers -- none at C1-C4 -- and is counted when it ran)
-PROBE_KERNELS = ("k_pass", "k_join_u")
-OPTIONAL_PROBE_KERNELS = ("k_join",)
+# probe phase: S partition passes + the LDS join (k_join_b for int64 rows,
+# k_join_u for i32 rows and probe-heavy joins; k_join takes the items they
+# defer -- none at C1-C4 -- and is counted when it ran)
+PROBE_KERNELS = ("k_pass",)
+FAST_JOIN_KERNELS = ("k_join_b", "k_join_u")
+OPTIONAL_PROBE_KERNELS = FAST_JOIN_KERNELS + ("k_join",)
 
 
 def parse():
@@ -403,7 +406,7 @@ def main():
         return round(b / (t_ms / 1000.0) / 1e9 / peak, 4) if t_ms > 0 else None
 
     roof = {
-        "scope": ("probe phase: S radix partition passes + k_join_u (SURVEY 8(d) t_probe)" if strategy == "radix"
+        "scope": ("probe phase: S radix partition passes + the LDS join (SURVEY 8(d) t_probe)" if strategy == "radix"
                   else "probe phase: k_probe + k_probe_slow (global table)"),
         "bound": "hbm",
         "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
@@ -420,11 +423,13 @@ def main():
     }
     if not use_dist and strategy == "radix":
         kbytes = (nr + ns) * (16 if wide else 8) + m_local * PAIR
-        roof["kernel"] = {"name": "k_join_u (hj_radix.hip; + k_join over deferred items)",
+        ran = [k for k in FAST_JOIN_KERNELS if rec and k in rec.get("kernels", {})]
+        roof["kernel"] = {"name": (ran[0] if ran else "k_join_b / k_join_u")
+                          + " (hj_radix.hip; + k_join over deferred items)",
                           "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
                           if join_ms > 0 else None, "frac": frac(kbytes, join_ms),
                           "algorithmic_bytes_per_launch": kbytes, "avg_launch_ms": round(join_ms, 4),
-                          "traffic": traffic_of(rec, ("k_join_u",)) if rec else None}
+                          "traffic": traffic_of(rec, (), FAST_JOIN_KERNELS) if ran else None}
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),

@@ -1741,6 +1741,413 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     }
 }
 
+// k_join_b: k_join_u's item loop, loads, defer rules and output compaction
+// over a BUCKETED LDS table (4 slots per bucket, 1024 buckets, a count per
+// bucket) instead of linear probing -- wide rows, the fast shape
+// (profiles/r02_join_cost_structure.txt: k_join_u's CAS walks and probe
+// chains are most of its time).
+//   build  = one returning LDS add on the home bucket's count per row (rank
+//            < 4: the slot; else the next bucket, and so on -- rare at load
+//            0.5), then plain stores of key and payload; no EMPTY marker,
+//            no table fill (the counts say which slots are live)
+//   dups   = every row ORs a 1-of-32 fingerprint of its key into its home
+//            bucket's signature (returning LDS or); a row that finds its
+//            bit already set is a suspect, and after the build each suspect
+//            (~3 % of the rows when keys are unique) looks for another live
+//            slot holding its key along its chain.  Exact: of c copies of a
+//            key all but the first to OR its bit are suspects and each finds
+//            a twin; a suspect without a twin is a fingerprint collision.
+//   probe  = the home bucket's count and its 4 keys (two 16-B reads), all
+//            rows' reads in flight together; a bucket whose count exceeds 4
+//            had a row pass it, so the walk goes on to the next bucket.
+// A bucket's count keeps growing as rows pass it (<= 4096: no overflow).
+template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, int ABL = 0>
+__global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;
+    constexpr int TS = 4096;
+    constexpr int BW = 4;
+    constexpr int NB = TS / BW;
+    constexpr unsigned kBMask = NB - 1;
+    constexpr int NW = NT / 64;
+    constexpr unsigned rb = (unsigned)(NW * RI);
+    constexpr unsigned subb = (unsigned)(NW * SI);
+    constexpr unsigned rmax = (unsigned)TS >> kRunLog;
+    constexpr unsigned rmax_rows = (unsigned)(TS * 3 / 4);
+    static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
+    constexpr unsigned kNone = 0xFFFFFFFFu;
+    __shared__ __attribute__((aligned(16))) u64 tkey[TS];
+    __shared__ __attribute__((aligned(16))) u64 tpay[WIDE ? TS : 2];
+    __shared__ __attribute__((aligned(16))) unsigned bcnt[NB];
+    __shared__ __attribute__((aligned(16))) unsigned bsig[NB];   // home bucket: OR of its rows' key fingerprints
+    constexpr unsigned kSusCap = 512;
+    __shared__ unsigned sus[kSusCap];   // suspect slots: slot | home bucket << 16
+    __shared__ u64 s_base;
+    __shared__ __attribute__((aligned(16))) unsigned s_ctl[4];   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
+    unsigned &s_bad = s_ctl[0], &s_dup = s_ctl[1], &s_rows = s_ctl[2], &s_nsus = s_ctl[3];
+    __shared__ unsigned s_cw[SI * NW];
+    __shared__ u64 wsum[16];
+    bool dup_sent = false;
+
+    const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
+    unsigned w = blockIdx.x;
+    if (w >= total) return;
+    const T *rrows = (const T *)a.r;
+    const T *srows = (const T *)a.s;
+    PT *orr = (PT *)a.out_r;
+    PT *oss = (PT *)a.out_s;
+    // the 10 hash bits above the LDS slot's low 2 (a.tshift is set for 12 bits)
+    const unsigned bsh = a.tshift + 2u;
+    const unsigned fsh = a.tshift - 5u;   // (a.tshift >= 28: 64 - <= 24 partition bits - 12)
+    auto bucket = [&](u64 key) { return (unsigned)(rhash(key) >> bsh) & kBMask; };
+    auto kof = [&](u64 e) { return WIDE ? e : (e >> 32); };
+    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
+    const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
+    const int lane = threadIdx.x & 63;
+    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const u64 li = lo + (u64)i * NW + wv0;
+            e[i] = li < hi ? sload(list + li) : 0ull;
+        }
+    };
+    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
+        unsigned ok = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            const bool in = off < (unsigned)(e[i] & 127u);
+            v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + (in ? off : 0u));
+            ok |= (unsigned)in << i;
+        }
+        return ok;
+    };
+    // live keys of bucket b: its count (capped at BW) and its 4 slots
+    auto read_bucket = [&](unsigned b, unsigned &c, u64 *k4) {
+        c = bcnt[b];
+        const ulonglong2 q0 = ((const ulonglong2 *)tkey)[b * 2], q1 = ((const ulonglong2 *)tkey)[b * 2 + 1];
+        k4[0] = q0.x;
+        k4[1] = q0.y;
+        k4[2] = q1.x;
+        k4[3] = q1.y;
+    };
+    T sv_[SI], rv_[RI];
+    u64 er[RI], es[SI];
+    ItemDesc it = sload(a.desc + w);
+    ents(a.r_runs, it.r_lo, it.r_hi, er, RI);
+    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    while (true) {
+        const bool fits = it.r_hi - it.r_lo <= (u64)rmax;
+        unsigned rok = 0, sok = 0;
+        if (fits) {
+            rok = rows_of(rrows, er, rv_, RI);
+            sok = rows_of(srows, es, sv_, SI);
+        }
+        const bool more = w + gridDim.x < total;
+        u64 ner[RI], nes[SI];
+        ItemDesc nx = it;
+        if (more) {
+            nx = sload(a.desc + w + gridDim.x);
+            ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
+            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+        }
+        if (!fits) {
+            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+        } else {
+            // (zeros from the item's descriptor -- r_lo < 2^63 -- or the
+            // compiler keeps a constant zero quad live across the loop and
+            // spills it)
+            const unsigned z = (unsigned)(it.r_lo >> 63);
+            const uint4 z4 = make_uint4(z, z, z, z);
+            // (thread 0 clears the control words: it is also the one that
+            // reads the previous item's s_dup after the item's last barrier)
+            static_assert(NB / 2 <= NT, "one 16-B clear per thread: counts, signatures");
+            if (threadIdx.x < NB / 4) ((uint4 *)bcnt)[threadIdx.x] = z4;
+            else if (threadIdx.x < NB / 2) ((uint4 *)bsig)[threadIdx.x - NB / 4] = z4;
+            if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
+            __syncthreads();
+            // ---- build: every row's rank add issued before any is used
+            bool bad = false;
+            for (u64 r0 = it.r_lo;;) {
+                unsigned bb[RI], rk[RI], susm = 0u;   // susm bit i: row i's fingerprint was set
+#pragma unroll
+                for (int i = 0; i < RI; ++i) {
+                    const u64 key = R::key(rv_[i]);
+                    bool act = (rok >> i) & 1u;
+                    if (WIDE && act && key == kEmptyKey64) {   // the null pass lives in k_join
+                        bad = true;
+                        act = false;
+                    }
+                    const u64 hh = rhash(key);
+                    bb[i] = (unsigned)(hh >> bsh) & kBMask;
+                    rk[i] = act ? atomicAdd(&bcnt[bb[i]], 1u) : 0u;
+                    const unsigned fp = 1u << ((unsigned)(hh >> fsh) & 31u);
+                    if (!(ABL & 2) && act && (atomicOr(&bsig[bb[i]], fp) & fp)) susm |= 1u << i;
+                    if (!act) rok &= ~(1u << i);
+                }
+                {
+                    unsigned wn = 0;
+#pragma unroll
+                    for (int i = 0; i < RI; ++i) wn += (unsigned)__popcll(__ballot((rok >> i) & 1u));
+                    if (lane == 0 && wn && atomicAdd(&s_rows, wn) + wn > rmax_rows) s_bad = 1u;
+                }
+#pragma unroll
+                for (int i = 0; i < RI; ++i) {
+                    if (!((rok >> i) & 1u)) continue;
+                    const unsigned home = bb[i];
+                    // a full bucket: the next one (the table never fills:
+                    // <= rmax_rows rows, else the item is deferred and a
+                    // full table's walk is cut at NB buckets)
+                    for (unsigned g = 0; rk[i] >= (unsigned)BW && g < (unsigned)NB; ++g) {
+                        bb[i] = (bb[i] + 1u) & kBMask;
+                        rk[i] = atomicAdd(&bcnt[bb[i]], 1u);
+                    }
+                    if (rk[i] >= (unsigned)BW) {   // (only past rmax_rows: deferred)
+                        s_bad = 1u;
+                        continue;
+                    }
+                    const unsigned slot = bb[i] * BW + rk[i];
+                    if constexpr (WIDE) {
+                        tkey[slot] = R::key(rv_[i]);
+                        tpay[slot] = R::pay(rv_[i]);
+                    } else {
+                        tkey[slot] = rv_[i];
+                    }
+                    if ((susm >> i) & 1u) {
+                        const unsigned q = atomicAdd(&s_nsus, 1u);
+                        if (q < kSusCap) sus[q] = slot | home << 16;
+                        else s_bad = 1u;   // (this many: k_join)
+                    }
+                }
+                r0 += rb;
+                if (r0 >= it.r_hi) break;
+                ents(a.r_runs, r0, it.r_hi, er, RI);
+                rok = rows_of(rrows, er, rv_, RI);
+            }
+            if (bad) s_bad = 1u;
+            __syncthreads();
+            bool early = false;   // (see below)
+            if (s_bad) {
+                if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            } else {
+            // ---- repeated build keys: each suspect looks for another live
+            // slot with its key along its chain (home bucket, then on while a
+            // bucket's count says a row passed it)
+            // Unique build keys leave ~rows^2 / (64 NB) suspects (fingerprint
+            // collisions in a home bucket); clearly more means repeats are
+            // likely, and then the verdict is waited for before the probe
+            // (no unique-path probe thrown away).  Either way it is exact.
+            const unsigned nsus = s_nsus, nrows = s_rows;
+            early = (u64)nsus * (64u * NB) * 2u > 3ull * nrows * nrows;
+            {
+                unsigned ndup = 0;
+                for (unsigned q = threadIdx.x; q < nsus && !(ABL & 1); q += NT) {
+                    const unsigned e = sus[q], slot = e & 0xFFFFu;
+                    unsigned h = e >> 16;
+                    const u64 key = kof(tkey[slot]);
+                    bool d = false;
+                    for (unsigned g = 0; g < (unsigned)NB; ++g) {
+                        unsigned c;
+                        u64 k4[BW];
+                        read_bucket(h, c, k4);
+#pragma unroll
+                        for (int j = 0; j < BW; ++j)
+                            d |= (unsigned)j < c && h * BW + (unsigned)j != slot && kof(k4[j]) == key;
+                        if (d || c <= (unsigned)BW) break;
+                        h = (h + 1u) & kBMask;
+                    }
+                    ndup += d ? 1u : 0u;
+                }
+                if (ndup) atomicAdd(&s_dup, ndup);
+            }
+            // (otherwise the suspects' verdict is read after the first
+            // sub-chunk's probe barrier: their walks overlap the probe's reads)
+            // Likely repeats: straight to the counting walks (exact for any
+            // keys); the suspects' verdict then only feeds the repeat flag,
+            // read after the item's last barrier.
+            bool known = early, unique = !early;
+                for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
+                    if (sb != it.s_lo) {
+                        ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
+                        sok = rows_of(srows, es, sv_, SI);
+                    }
+                    unsigned pm = 0u;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i)
+                        if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64)) pm |= 1u << i;
+                    // repeated build keys: each row counts its matches along
+                    // its chain, then walks it again writing at its prefix;
+                    // true: the item went to k_join (nothing written)
+                    auto gen_sub = [&](u64 sb, unsigned pm) -> bool {
+                        unsigned cnt = 0, mb = 0u;
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            if (!((pm >> i) & 1u)) continue;
+                            const u64 key = R::key(sv_[i]);
+                            unsigned h = bucket(key);
+                            const unsigned c0 = cnt;
+                            for (unsigned g = 0; g < (unsigned)NB; ++g) {
+                                unsigned c;
+                                u64 k4[BW];
+                                read_bucket(h, c, k4);
+#pragma unroll
+                                for (int j = 0; j < BW; ++j) cnt += ((unsigned)j < c && kof(k4[j]) == key) ? 1u : 0u;
+                                if (c <= (unsigned)BW) break;
+                                h = (h + 1u) & kBMask;
+                            }
+                            if (cnt != c0) mb |= 1u << i;
+                        }
+                        u64 tot;
+                        const u64 pre = block_excl_scan<NT>((u64)cnt, wsum, &tot);
+                        if (!WIDE && WRITE && sb == it.s_lo && tot > (u64)(2 * NT * SI)) {
+                            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+                            return true;
+                        }
+                        if constexpr (!WRITE) {
+                            if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
+                        } else if (tot) {
+                            if (threadIdx.x == 0) s_base = atomicAdd(a.counter, tot);
+                            __syncthreads();
+                            u64 pos = s_base + pre;
+#pragma unroll
+                            for (int i = 0; i < SI; ++i) {
+                                if (!((mb >> i) & 1u)) continue;
+                                const u64 key = R::key(sv_[i]);
+                                const PT spay = (PT)R::pay(sv_[i]);
+                                unsigned h = bucket(key);
+                                for (unsigned g = 0; g < (unsigned)NB; ++g) {
+                                    unsigned c;
+                                    u64 k4[BW];
+                                    read_bucket(h, c, k4);
+#pragma unroll
+                                    for (int j = 0; j < BW; ++j) {
+                                        if ((unsigned)j < c && kof(k4[j]) == key) {
+                                            if (pos < (u64)a.cap) {
+                                                orr[pos] = WIDE ? (PT)tpay[h * BW + j] : (PT)(k4[j] & 0xffffffffull);
+                                                oss[pos] = spay;
+                                            }
+                                            ++pos;
+                                        }
+                                    }
+                                    if (c <= (unsigned)BW) break;
+                                    h = (h + 1u) & kBMask;
+                                }
+                            }
+                        }
+                        __syncthreads();
+                        return false;
+                    };
+                    if (known && !unique) {
+                        if (gen_sub(sb, pm)) break;
+                        continue;
+                    }
+                    // unique build keys: the home bucket of every row read
+                    // before any is resolved
+                    unsigned m[SI], hb[SI], cb[SI];
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        m[i] = kNone;
+                        hb[i] = bucket(R::key(sv_[i]));
+                        cb[i] = 0u;
+                        if ((pm >> i) & 1u) {
+                            u64 k4[BW];
+                            read_bucket(hb[i], cb[i], k4);
+                            const u64 key = R::key(sv_[i]);
+#pragma unroll
+                            for (int j = BW - 1; j >= 0; --j)
+                                if ((unsigned)j < cb[i] && kof(k4[j]) == key) m[i] = hb[i] * BW + j;
+                        }
+                    }
+                    // rows whose home bucket was passed by a full one's rows
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        if (!((pm >> i) & 1u)) continue;
+                        const u64 key = R::key(sv_[i]);
+                        unsigned h = hb[i], c = cb[i];
+                        for (unsigned g = 0; m[i] == kNone && c > (unsigned)BW && g < (unsigned)NB; ++g) {
+                            h = (h + 1u) & kBMask;
+                            u64 k4[BW];
+                            read_bucket(h, c, k4);
+#pragma unroll
+                            for (int j = BW - 1; j >= 0; --j)
+                                if ((unsigned)j < c && kof(k4[j]) == key) m[i] = h * BW + j;
+                        }
+                    }
+                    const int wv = threadIdx.x >> 6;
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 bal = __ballot(m[i] != kNone);
+                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                    }
+                    __syncthreads();
+                    if (!known) {
+                        known = true;
+                        unique = s_dup == 0u;
+                        if (!unique) {
+                            if (!dup_sent) {   // once per workgroup (k_join)
+                                if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                dup_sent = true;
+                            }
+                            if (gen_sub(sb, pm)) break;
+                            continue;
+                        }
+                    }
+                    if (wv == 0) {
+                        constexpr int K = (SI * NW + 63) / 64;
+                        unsigned v[K], sum = 0;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int jj = lane * K + k;
+                            v[k] = jj < SI * NW ? s_cw[jj] : 0u;
+                            sum += v[k];
+                        }
+                        const unsigned x = wave_incl_add(sum);
+                        unsigned run = x - sum;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            const int jj = lane * K + k;
+                            if (jj < SI * NW) s_cw[jj] = run;
+                            run += v[k];
+                        }
+                        if (lane == 63 && x) {
+                            if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
+                            else atomicAdd(a.counter, (u64)x);
+                        }
+                    }
+                    if constexpr (WRITE) {
+                        __syncthreads();
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            const u64 bal = __ballot(m[i] != kNone);
+                            if (m[i] == kNone) continue;
+                            const u64 pos = s_base + s_cw[i * NW + wv] + (unsigned)__popcll(bal & lt);
+                            if (pos < (u64)a.cap) {
+                                st_s<kNtJoinSt>(orr + pos, WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull));
+                                st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
+                            }
+                        }
+                    }
+                    if (sb + subb < it.s_hi) __syncthreads();
+                }
+            }
+            __syncthreads();
+            // (early items: the repeat flag, once per workgroup)
+            if (threadIdx.x == 0 && early && !dup_sent && s_dup != 0u) {
+                __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dup_sent = true;
+            }
+        }
+        if (!more) break;
+        w += gridDim.x;
+        it = nx;
+#pragma unroll
+        for (int i = 0; i < RI; ++i) er[i] = ner[i];
+#pragma unroll
+        for (int i = 0; i < SI; ++i) es[i] = nes[i];
+    }
+}
+
 // --------------------------------------------------------------- grouped join
 // k_join_grp: narrow rows (the reference's i32 keys / row ids) whose build
 // keys repeat many times -- join-performances.md:3-6's 10M x 10M keys in
@@ -2309,7 +2716,8 @@ __global__ __launch_bounds__(NT, 4) void k_join2(JoinArgs a) {
 // Join kernel variant.  Default (kind 0): k_join_u, 768 threads, 3 build +
 // 3 probe rows per thread, 6 waves per SIMD, with k_join over the items it
 // defers (profiles/r02_join_fast.txt: C3 k_join 3.50 -> 2.81 ms, C2 12.34 ->
-// 9.45 ms, C1-ref 1.31 -> 0.96 ms).  HJ_JOIN=1 runs k_join alone (HJ_JOIN_TSL
+// 9.45 ms, C1-ref 1.31 -> 0.96 ms); int64 rows in that shape take k_join_b,
+// its bucketed-table form (C3 2.77 -> 2.55 ms; HJ_JOIN_BKT=0: k_join_u).  HJ_JOIN=1 runs k_join alone (HJ_JOIN_TSL
 // 11 | 12 | 13 picks its table), HJ_JOIN=2 the bucketized k_join2, 3 / 4
 // k_join's register-prefetch variants (all measured slower: DESIGN.md 4).
 struct JoinVariant {
@@ -2342,6 +2750,15 @@ JoinVariant join_variant() {
     if (kind == 3) return JoinVariant{13, 512, 3, 5};   // prefetching k_join, 1 workgroup per CU, 8192 slots
     if (kind == 4) return JoinVariant{12, 512, 4, 3};   // prefetching k_join, 2 workgroups per CU, 3 S rows
     return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256), 1, kJoinItems};
+}
+
+// wide rows, fast shape: the bucketed table (k_join_b) unless HJ_JOIN_BKT=0
+bool join_bucketed() {
+    static bool on = [] {
+        const char *e = getenv("HJ_JOIN_BKT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 int cu_count() {
@@ -2624,9 +3041,14 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                 hipLaunchKernelGGL((k_join_u<true, WR, 12, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),   \
                                    dim3(grid), dim3(kStreamNT), 0, st, a);                                 \
         }                                                                                                  \
-        if (!st_)                                                                                          \
-            hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),      \
-                               dim3(kFastNT), 0, st, a);                                                   \
+        if (!st_) {                                                                                        \
+            if (W && join_bucketed())                                                                      \
+                hipLaunchKernelGGL((k_join_b<true, WR, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),   \
+                                   dim3(kFastNT), 0, st, a);                                               \
+            else                                                                                           \
+                hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),  \
+                                   dim3(kFastNT), 0, st, a);                                               \
+        }                                                                                                  \
     } while (0)
 #define HJ_JOINGRP(WR, LST) \
     hipLaunchKernelGGL((k_join_grp<WR, kGrpNT, kGrpRI, kGrpSI, LST>), dim3(grid), dim3(kGrpNT), 0, st, a)
