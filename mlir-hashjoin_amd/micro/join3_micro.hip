@@ -148,7 +148,7 @@ int body(int lg) {
         run("768 thr 3+3, 8192 slots", [&] { hipLaunchKernelGGL((k_join_u<W, true, 13, 768, 3, 3, 6>), dim3(2 * cus), dim3(768), 0, 0, a); });
         a.tshift = 64 - pl.total_bits - 12;
     }
-    if (W) {
+    {
         run("k_join_b", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6>), dim3(2 * cus), dim3(768), 0, 0, a); });
         run("k_join_b, no suspect checks", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6, 1>), dim3(2 * cus), dim3(768), 0, 0, a); });
         run("k_join_b, no signatures", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6, 2>), dim3(2 * cus), dim3(768), 0, 0, a); });
