@@ -163,7 +163,7 @@ struct hj_ctx {
     // reference's 10M x 10M keys in [1, 100k]), the next joins skip the fast
     // path (narrow rows: k_join_grp over every item), re-checking it every
     // kFastRecheck joins.
-    unsigned *join_stats = nullptr;       // host-mapped pinned, 2 words
+    unsigned *join_stats = nullptr;       // host-mapped pinned, 3 words (+ [2]: k_join_b saw repeated build keys)
     unsigned *join_stats_dev = nullptr;
     unsigned long long joins = 0;
     static constexpr unsigned kFastRecheck = 8;
@@ -407,9 +407,9 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         record(c, kEvProbeMid, st);
         if (!c->join_stats) {
             void *hp = nullptr;
-            HJ_HIP(hipHostMalloc(&hp, 2 * sizeof(unsigned), hipHostMallocMapped));
+            HJ_HIP(hipHostMalloc(&hp, 3 * sizeof(unsigned), hipHostMallocMapped));
             c->join_stats = (unsigned *)hp;
-            c->join_stats[0] = c->join_stats[1] = 0u;
+            c->join_stats[0] = c->join_stats[1] = c->join_stats[2] = 0u;
             void *dp = nullptr;
             HJ_HIP(hipHostGetDevicePointer(&dp, hp, 0));
             c->join_stats_dev = (unsigned *)dp;
@@ -418,11 +418,17 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         const unsigned deferred = ((volatile unsigned *)c->join_stats)[0];
         const unsigned items = ((volatile unsigned *)c->join_stats)[1];
         const bool general = items > 0 && 2ull * deferred > items && (c->joins % hj_ctx::kFastRecheck) != 0;
+        // int64 rows: the bucketed join (k_join_b) unless the last one found
+        // repeated build keys (its counting walks lose to k_join_u's there,
+        // C1-ref); re-tried every kFastRecheck joins like the fast path
+        const bool repeated = ((volatile unsigned *)c->join_stats)[2] != 0u;
+        const bool bucketed = !repeated || (c->joins % hj_ctx::kFastRecheck) == 0;
+        if (bucketed) ((volatile unsigned *)c->join_stats)[2] = 0u;
         ++c->joins;
         HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
                               (unsigned long long *)d_count, c->meta + 1, count_only, st, c->join_stats_dev, general,
-                              src.n >= 8 * c->n_build));
+                              src.n >= 8 * c->n_build, bucketed));
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;

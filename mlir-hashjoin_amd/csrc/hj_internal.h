@@ -185,11 +185,14 @@ size_t radix_item_desc_bytes();
 // {items deferred by the fast path, items}; general = skip the fast path
 // (k_join over every item), chosen by the caller when the last join on the
 // context deferred most of its items; stream = the probe side is many times
-// the build side (C2): the fast path's larger-sub-chunk shape.
+// the build side (C2): the fast path's larger-sub-chunk shape; bucketed =
+// int64 rows may take k_join_b (the caller passes false after a join whose
+// build keys repeated: join_stats[2], written by k_join_b).
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats = nullptr, bool general = false, bool stream = false);
+                      unsigned *join_stats = nullptr, bool general = false, bool stream = false,
+                      bool bucketed = true);
 
 // Routing fan-out limit: k_part_scatter (> 512 parts) keeps 12 B of LDS
 // counters per part, k_part_hist 4 B (<= 96 KiB of the 160 KiB).

@@ -849,6 +849,7 @@ struct JoinArgs {
     unsigned *defer = nullptr, *defer_n = nullptr;
     const unsigned *list = nullptr, *list_n = nullptr;
     unsigned *stats = nullptr;       // list mode: {deferred items, items} for the caller's next choice
+    unsigned *rep = nullptr;         // k_join_b: set to 1 (host-mapped) when its build keys repeat
 };
 
 struct ItemDesc {
@@ -2086,7 +2087,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         unique = s_dup == 0u;
                         if (!unique) {
                             if (!dup_sent) {   // once per workgroup (k_join)
-                                if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                if (threadIdx.x == 0) {
+                    __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (a.rep) __hip_atomic_store(a.rep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
                                 dup_sent = true;
                             }
                             if (gen_sub(sb, pm)) break;
@@ -2135,6 +2139,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             // (early items: the repeat flag, once per workgroup)
             if (threadIdx.x == 0 && early && !dup_sent && s_dup != 0u) {
                 __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (a.rep) __hip_atomic_store(a.rep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 dup_sent = true;
             }
         }
@@ -2974,7 +2979,7 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats, bool general, bool stream) {
+                      unsigned *join_stats, bool general, bool stream, bool bucketed) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     const JoinVariant jv = join_variant();
@@ -3042,7 +3047,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                                    dim3(grid), dim3(kStreamNT), 0, st, a);                                 \
         }                                                                                                  \
         if (!st_) {                                                                                        \
-            if (W && join_bucketed())                                                                      \
+            if (W && bucketed && join_bucketed())                                                          \
                 hipLaunchKernelGGL((k_join_b<true, WR, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),   \
                                    dim3(kFastNT), 0, st, a);                                               \
             else                                                                                           \
@@ -3055,6 +3060,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     if (fast) {
         a.defer = defer_n + 1;
         a.defer_n = defer_n;
+        a.rep = join_stats ? join_stats + 2 : nullptr;
         if (wide) {
             if (count_only) HJ_JOINU(true, false);
             else HJ_JOINU(true, true);
