@@ -356,3 +356,24 @@ def test_radix_bucketed_table_repeat_detection(hj, oracle, rows, bits, dups):
     o = run(hj, rk, rp, sk, sp, bits)
     assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
     assert hj.has_duplicates() == (dups != "none")
+
+
+def test_wide_join_choice_after_repeats(oracle):
+    """A context whose bucketed join (k_join_b) found repeated int64 build
+    keys runs the next joins with k_join_u (re-trying k_join_b every 8th):
+    results and the repeat flag stay exact across the switches."""
+    h = HashJoin(0)
+    try:
+        rk_u, rp_u, sk_u, sp_u = oracle.gen_pkfk_i64(41, 150000, 150000, 0.9)
+        rk_d, rp_d = oracle.gen_uniform_i64(42, 1, 1, 1 << 30, 150000)
+        sk_d, sp_d = oracle.gen_uniform_i64(42, 2, 1, 1 << 30, 150000)
+        rk_d[:3000] = rk_d[3000:6000]   # some repeats in every partition
+        want_u = oracle.chained_join_i64(rk_u, rp_u, sk_u, sp_u, H=1000)
+        want_d = oracle.chained_join_i64(rk_d, rp_d, sk_d, sp_d, H=1000)
+        for i, dup in enumerate([True, False, False, True] + [False] * 6):
+            rk, rp, sk, sp, want = (rk_d, rp_d, sk_d, sp_d, want_d) if dup else (rk_u, rp_u, sk_u, sp_u, want_u)
+            o = run(h, rk, rp, sk, sp, 6)
+            assert oracle.same_multiset(*o, *want), f"join {i}"
+            assert h.has_duplicates() == dup, f"join {i}"
+    finally:
+        h.close()
