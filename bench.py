@@ -426,7 +426,8 @@ def main():
         ran = [k for k in FAST_JOIN_KERNELS if rec and k in rec.get("kernels", {})]
         # (without a PMC record: int64 rows take k_join_b unless the probe side
         # is >= 8x the build side, i32 rows k_join_u / k_join_grp)
-        guess = "k_join_b" if (wide and ns < 8 * nr) else ("k_join_u" if wide else "k_join_u / k_join_grp")
+        guess = ("k_join_b (k_join_u after repeated build keys)" if (wide and ns < 8 * nr)
+                 else ("k_join_u" if wide else "k_join_u / k_join_grp"))
         roof["kernel"] = {"name": (ran[0] if ran else guess)
                           + " (hj_radix.hip; + k_join over deferred items)",
                           "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
