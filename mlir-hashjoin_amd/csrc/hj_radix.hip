@@ -1762,6 +1762,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 //            rows' reads in flight together; a bucket whose count exceeds 4
 //            had a row pass it, so the walk goes on to the next bucket.
 // A bucket's count keeps growing as rows pass it (<= 4096: no overflow).
+// The product launches it for int64 rows only (i32 rows keep k_join_u, where
+// their many-repeat deferral to k_join_grp lives).  ABL (micro/join3_micro.hip
+// ablations only; 0 in the product): bit 0 no suspect checks, bit 1 no
+// fingerprints (timing only).
 template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, int ABL = 0>
 __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     typedef Row<WIDE> R;
