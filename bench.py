@@ -15,8 +15,10 @@ join of the whole relations with inputs resident in HBM:
 value = |S| / (time per step), the whole job over all ranks (max over ranks).
 `roofline` is SURVEY 8(d)'s probe-phase figure: 48 B per probe tuple (16 B S
 row + 16 B slot + 16 B output pair) over the probe phase's HIP-event time;
-`roofline.kernel` is the same for the dominant kernel (the LDS join: k_join_b
-for int64 rows, k_join_u for i32 rows and probe-heavy joins) alone.
+`roofline.read_frac` counts the probe phase's READ bytes only (16 B S row +
+16 B slot per probe tuple: north_star's "HBM read roofline").
+`roofline.kernel` is the same for the dominant kernel (the LDS join: the one
+hj_ctx_join_kernel names -- k_join_b / k_join_u / k_join_grp) alone.
 Launch:  python bench.py [--gpus 1 --steps K --warmup W --config C3]
          python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
@@ -57,11 +59,11 @@ REFERENCE_PUBLISHED = {
     "REF-A": {"join_v1_s": 2.0, "join_v2_s": 1.5, "source": "join-performances.md:3-6, :16-19"},
     "REF-B": {"join_v1_s": 12.0, "join_v2_s": 12.5, "source": "join-performances.md:8-11, :21-24"},
 }
-# probe phase: S partition passes + the LDS join (k_join_b for int64 rows,
-# k_join_u for i32 rows and probe-heavy joins; k_join takes the items they
-# defer -- none at C1-C4 -- and is counted when it ran)
+# probe phase: S partition passes + the LDS join (hj_ctx_join_kernel: k_join_b /
+# k_join_u / k_join_grp; k_join takes the items they defer -- none at C1-C4 --
+# and is counted when it ran; the kernels not chosen exit at once)
 PROBE_KERNELS = ("k_pass",)
-FAST_JOIN_KERNELS = ("k_join_b", "k_join_u")
+FAST_JOIN_KERNELS = ("k_join_b", "k_join_u", "k_join_grp")
 OPTIONAL_PROBE_KERNELS = FAST_JOIN_KERNELS + ("k_join",)
 
 
@@ -396,9 +398,11 @@ def main():
     build_ms = (phases["init"] + phases["build"]) / a.steps
     strategy = hj.strategy_used or a.strategy
     probe_bytes = ns * (K + SLOT) + m_local * PAIR
+    read_bytes = ns * (K + SLOT)
     if use_dist:
         nr_loc, ns_loc = last["rows"]
         probe_bytes = ns_loc * (K + SLOT) + m_local * PAIR
+        read_bytes = ns_loc * (K + SLOT)
     rec, traffic_note = pmc_record(a.config, world)
     info = hashjoin.device_info(local)
 
@@ -419,21 +423,24 @@ def main():
         "bytes_per_probe_row": round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2),
         "ms": round(probe_ms, 4),
         "frac_of_achievable": frac(probe_bytes, probe_ms, HBM_ACHIEVABLE_GBS),
+        # north_star's "HBM read roofline": the probe phase's algorithmic READ
+        # bytes only (S row + one slot per probe tuple)
+        "read_bytes": read_bytes,
+        "read_frac": frac(read_bytes, probe_ms),
         "target": "north_star: frac >= 0.40 at |R|=|S|=2^28 (t_probe <= 4.0 ms)",
     }
     if not use_dist and strategy == "radix":
         kbytes = (nr + ns) * (16 if wide else 8) + m_local * PAIR
-        ran = [k for k in FAST_JOIN_KERNELS if rec and k in rec.get("kernels", {})]
-        # (without a PMC record: int64 rows take k_join_b unless the probe side
-        # is >= 8x the build side, i32 rows k_join_u / k_join_grp)
-        guess = ("k_join_b (k_join_u after repeated build keys)" if (wide and ns < 8 * nr)
-                 else ("k_join_u" if wide else "k_join_u / k_join_grp"))
-        roof["kernel"] = {"name": (ran[0] if ran else guess)
-                          + " (hj_radix.hip; + k_join over deferred items)",
+        # the kernel is a function of the data (row width, |S| / |R|, the build
+        # side's sampled repeats), reported by the context itself
+        kname = hj.join_kernel or "?"
+        kbase = kname.replace("_stream", "")
+        ran = [kbase] if rec and kbase in rec.get("kernels", {}) else []
+        roof["kernel"] = {"name": kname + " (hj_radix.hip; + k_join over deferred items)",
                           "achieved": round(kbytes / (join_ms / 1000.0) / 1e9, 1)
                           if join_ms > 0 else None, "frac": frac(kbytes, join_ms),
                           "algorithmic_bytes_per_launch": kbytes, "avg_launch_ms": round(join_ms, 4),
-                          "traffic": traffic_of(rec, (), FAST_JOIN_KERNELS) if ran else None}
+                          "traffic": traffic_of(rec, (), ran) if ran else None}
     line = {
         "metric": "probed tuples/sec + joined rows/sec, |R|=|S|=2^28 int64 keys",
         "value": round(value, 1),

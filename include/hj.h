@@ -115,6 +115,19 @@ int hj_ctx_last_timing(hj_ctx *ctx, float ms[4]);
 /* Same plus the probe's split: [4] probe-side partitioning (RADIX, else 0),
  * [5] probe/join kernel; [6], [7] reserved (-1). */
 int hj_ctx_last_timing_ex(hj_ctx *ctx, float ms[8]);
+/* RADIX: the join kernel of the last probe.  A pure function of the row
+ * width, the probe / build size ratio (>= 8: the probe-heavy shape) and the
+ * build side's repeated keys, sampled at build time over up to 64 partitions
+ * -- never of an earlier join's statistics: HJ_JOIN_KERNEL_BUCKETED
+ * (k_join_b), _LINEAR (k_join_u), _STREAM (k_join_u, probe-heavy shape),
+ * _GROUPED (k_join_grp over every item); 0 if the last probe was no radix
+ * join.  Items those kernels defer (INT64_MIN build keys, oversized
+ * partitions) run k_join afterwards.  Synchronises. */
+#define HJ_JOIN_KERNEL_BUCKETED 1
+#define HJ_JOIN_KERNEL_LINEAR 2
+#define HJ_JOIN_KERNEL_STREAM 3
+#define HJ_JOIN_KERNEL_GROUPED 4
+int hj_ctx_join_kernel(hj_ctx *ctx);
 
 /* ------------------------------------------------------------ device phases
  * build:  @initializeHashTable + @buildTable   (join_v2.mlir:54-108)

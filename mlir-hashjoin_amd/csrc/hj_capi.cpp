@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -142,31 +143,29 @@ struct hj_ctx {
     void *dbuf[kDbufs] = {};
     size_t dbuf_bytes[kDbufs] = {};
     unsigned long long *dcount = nullptr;
-    // count -> probe reuse (join_v1.mlir:110-176 builds once for @countRows
-    // and @probeRelation): the last host join's inputs stay in staging set
-    // `set` (dbuf[6 + 2 set], dbuf[7 + 2 set]) and its pairs in dbuf[2],
-    // dbuf[3]; the next call uploads into the other set and, when the bytes
-    // are identical (compared on the device), returns the same pairs without
-    // building or probing again.
+    // count -> probe reuse (join_v1.mlir:110-176: @countRows leaves its table
+    // for @probeRelation).  hj_count_* uploads both relations into dbuf[6],
+    // dbuf[7], builds, and COUNTS (no pairs); it keeps the built table, the
+    // staged probe side and a content digest of each input memref.  The next
+    // hj_probe_* digests its memrefs on the host (no upload) and, when both
+    // digests match, only probes into M-row buffers and downloads.  Any other
+    // build on the context invalidates it.
+    struct Digest {
+        unsigned long long a = 0, b = 0;
+        bool operator==(const Digest &o) const { return a == o.a && b == o.b; }
+    };
     struct Memo {
         bool valid = false;
-        int kind = 0;                      // 32 | 64 (payload columns: 64 + 1 if given)
-        size_t bytes_r = 0, bytes_s = 0;   // uploaded bytes per side
-        int set = 0;
+        int layout = -1;
+        int64_t nr = 0, ns = 0;
+        Digest dr, ds;   // R (keys, payloads), S (keys, payloads)
         int64_t m = 0;
     } memo;
     long long memo_hits = 0;
-    // radix join kernel choice: the fast path (k_join_u) defers items it
-    // cannot take to k_join (narrow rows: to k_join_grp first); the list-mode
-    // launch leaves {deferred, items} in join_stats (host-mapped).  When the
-    // last fast join deferred most of its items (keys that mostly repeat: the
-    // reference's 10M x 10M keys in [1, 100k]), the next joins skip the fast
-    // path (narrow rows: k_join_grp over every item), re-checking it every
-    // kFastRecheck joins.
-    unsigned *join_stats = nullptr;       // host-mapped pinned, 3 words (+ [2]: k_join_b saw repeated build keys)
-    unsigned *join_stats_dev = nullptr;
-    unsigned long long joins = 0;
-    static constexpr unsigned kFastRecheck = 8;
+    // the last radix probe's shape, for hj_ctx_join_kernel (the kernel itself
+    // follows from these and the build-time sample in meta[2..3])
+    bool join_ran = false, join_wide = false, join_stream = false;
+    hipStream_t join_st = nullptr;
 };
 
 namespace {
@@ -320,6 +319,8 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->n_build = src.n;
     c->used = choose_strategy(c, src.n);
     c->probe_used = -1;
+    c->join_ran = false;
+    c->memo.valid = false;   // (hj_count_*'s kept table is gone)
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
@@ -329,10 +330,13 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         c->plan = hj::radix_plan(src.n, c->radix_bits);
         HJ_TRY(ensure_radix_scratch(c, c->rset, src.n, esz, c->plan));
         record(c, kEvInit0, st);
-        HJ_HIP(hipMemsetAsync(c->meta, 0, 2 * sizeof(unsigned long long), st));
+        // meta[0] side count, [1] dup flag, [2..3] the build-side sample
+        HJ_HIP(hipMemsetAsync(c->meta, 0, 4 * sizeof(unsigned long long), st));
         record(c, kEvInit1, st);
         trace("build: workspace", st, src.n);
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->rset), st));
+        // repeated build keys, sampled: decides the join kernel (radix_join)
+        HJ_HIP(hj::radix_sample(wide, c->plan, bucket_set(c->rset), c->meta + 2, st));
         trace("build: R partitioned", st, (long long)c->plan.total_bits);
         if (!c->dual) {
             record(c, kEvBuild1, st);
@@ -395,6 +399,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
     const bool radix = c->used == HJ_STRATEGY_RADIX || (c->dual && src.n >= kRadixProbeMinRows);
     c->probe_used = radix ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
+    c->join_ran = false;
     if (radix) {
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;
@@ -405,30 +410,15 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
-        if (!c->join_stats) {
-            void *hp = nullptr;
-            HJ_HIP(hipHostMalloc(&hp, 3 * sizeof(unsigned), hipHostMallocMapped));
-            c->join_stats = (unsigned *)hp;
-            c->join_stats[0] = c->join_stats[1] = c->join_stats[2] = 0u;
-            void *dp = nullptr;
-            HJ_HIP(hipHostGetDevicePointer(&dp, hp, 0));
-            c->join_stats_dev = (unsigned *)dp;
-        }
-        // (read without waiting: the values of whichever fast join finished last)
-        const unsigned deferred = ((volatile unsigned *)c->join_stats)[0];
-        const unsigned items = ((volatile unsigned *)c->join_stats)[1];
-        const bool general = items > 0 && 2ull * deferred > items && (c->joins % hj_ctx::kFastRecheck) != 0;
-        // int64 rows: the bucketed join (k_join_b) unless the last one found
-        // repeated build keys (its counting walks lose to k_join_u's there,
-        // C1-ref); re-tried every kFastRecheck joins like the fast path
-        const bool repeated = ((volatile unsigned *)c->join_stats)[2] != 0u;
-        const bool bucketed = !repeated || (c->joins % hj_ctx::kFastRecheck) == 0;
-        if (bucketed) ((volatile unsigned *)c->join_stats)[2] = 0u;
-        ++c->joins;
+        // the kernel: a function of (row width, size ratio, build-time sample)
+        const bool stream = src.n >= 8 * c->n_build;
         HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
-                              (unsigned long long *)d_count, c->meta + 1, count_only, st, c->join_stats_dev, general,
-                              src.n >= 8 * c->n_build, bucketed));
+                              (unsigned long long *)d_count, c->meta + 1, count_only, st, c->meta + 2, stream));
+        c->join_ran = true;
+        c->join_wide = wide;
+        c->join_stream = stream;
+        c->join_st = st;
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
@@ -644,40 +634,119 @@ int host_stream(hj_ctx *c) {
     return HJ_OK;
 }
 
-// Staging set for the next host join's inputs (the other one holds the
-// memoised join's inputs).
-int next_set(const hj_ctx *c) { return c->memo.valid ? c->memo.set ^ 1 : 0; }
-
-// true when the `bytes` at device pointers a and b are identical
-int same_bytes(hj_ctx *c, const void *a, const void *b, size_t bytes, bool *eq) {
-    *eq = true;
-    if (bytes == 0) return HJ_OK;
-    HJ_HIP(hipMemsetAsync(c->dcount + 1, 0, sizeof(unsigned long long), c->host_stream));
-    HJ_HIP(hj::launch_memeq(a, b, bytes, c->dcount + 1, c->host_stream));
-    unsigned long long ne = 0;
-    HJ_HIP(hipMemcpyAsync(&ne, c->dcount + 1, 8, hipMemcpyDeviceToHost, c->host_stream));
-    HJ_HIP(hipStreamSynchronize(c->host_stream));
-    *eq = ne == 0;
-    return HJ_OK;
+// ---- content digests of host memrefs (count -> probe reuse)
+// 128 bits from four multiply-rotate lanes over the elements' bytes (lane j
+// takes every 4th 8-B word), cut into up to 8 chunks hashed on host threads;
+// a changed element changes its lane's state, which no later word undoes
+// except by a crafted value.  Memory-bound: ~2^29 B (two 2^24-row int64
+// relations) in ~10 ms, overlapped with the upload in hj_count_*.
+typedef hj_ctx::Digest Digest;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t dstep(uint64_t h, uint64_t w) { return rotl64((h ^ w) * 0x9E3779B97F4A7C15ull, 31); }
+inline uint64_t fmix(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 33;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    return k ^ (k >> 33);
 }
 
-// The memoised join (same kind, byte-identical inputs in set `y`)?
-int memo_hit(hj_ctx *c, int kind, int y, size_t br, size_t bs, bool *hit) {
-    *hit = false;
-    const hj_ctx::Memo &mm = c->memo;
-    if (!mm.valid || mm.kind != kind || mm.bytes_r != br || mm.bytes_s != bs) return HJ_OK;
-    bool eq = false;
-    HJ_TRY(same_bytes(c, c->dbuf[6 + 2 * mm.set], c->dbuf[6 + 2 * y], br, &eq));
-    if (eq) HJ_TRY(same_bytes(c, c->dbuf[7 + 2 * mm.set], c->dbuf[7 + 2 * y], bs, &eq));
-    *hit = eq;
-    return HJ_OK;
+Digest digest_mem(const void *aligned, int64_t off, int64_t size, int64_t stride, int esz) {
+    Digest d;
+    d.a = fmix((uint64_t)size * 16 + (uint64_t)esz);
+    d.b = fmix(d.a ^ 0x5EEDull);
+    if (size <= 0 || !aligned) return d;
+    const char *base = (const char *)aligned + off * esz;
+    const int64_t bytes = size * esz;
+    const unsigned hw = std::thread::hardware_concurrency();
+    unsigned T = (unsigned)(bytes >> 22) + 1;   // >= 4 MiB per thread
+    if (T > 8) T = 8;
+    if (hw && T > hw) T = hw;
+    std::vector<Digest> part(T);
+    auto work = [&](unsigned t) {
+        const int64_t e0 = size * t / T, e1 = size * (t + 1) / T;
+        uint64_t h[4] = {0x243F6A8885A308D3ull, 0x13198A2E03707344ull, 0xA4093822299F31D0ull, 0x082EFA98EC4E6C89ull};
+        if (stride == 1) {
+            const char *p = base + e0 * esz;
+            const size_t n = (size_t)(e1 - e0) * (size_t)esz;
+            size_t i = 0;
+            for (; i + 32 <= n; i += 32) {
+                uint64_t w[4];
+                std::memcpy(w, p + i, 32);
+                for (int j = 0; j < 4; ++j) h[j] = dstep(h[j], w[j]);
+            }
+            uint64_t w[4] = {0, 0, 0, 0};
+            std::memcpy(w, p + i, n - i);
+            for (int j = 0; j < 4; ++j) h[j] = dstep(h[j], w[j] ^ (uint64_t)(n - i));
+        } else {
+            for (int64_t e = e0; e < e1; ++e) {
+                uint64_t w = 0;
+                std::memcpy(&w, base + e * stride * esz, (size_t)esz);
+                h[e & 3] = dstep(h[e & 3], w);
+            }
+        }
+        part[t].a = fmix(h[0]) ^ fmix(h[1] + 0x9E3779B97F4A7C15ull);
+        part[t].b = fmix(h[2]) ^ fmix(h[3] + 0x9E3779B97F4A7C15ull);
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    for (unsigned t = 0; t < T; ++t) {
+        d.a = fmix(d.a ^ part[t].a) + t;
+        d.b = fmix(d.b ^ part[t].b) + t;
+    }
+    return d;
 }
 
-// Probe into dbuf[2] / dbuf[3] sized optimistically (|S| rows), once more at
-// the exact M when that was too small; *m = M.
-int host_probe_all(hj_ctx *c, int layout, const hj::SrcDev &probe, size_t esz, int64_t ns, int64_t *m) {
+// One host relation of the memref ABI: a key column and (int64 rows) an
+// optional payload column (null: payload = row id, the reference's rowId,
+// join_v1.mlir:255).
+struct HostRel {
+    const void *k;
+    int64_t k_off, k_stride;
+    const void *p;
+    int64_t p_off, p_stride;
+    int64_t n;
+};
+
+Digest digest_rel(const HostRel &r, int esz) {
+    Digest d = digest_mem(r.k, r.k_off, r.n, r.k_stride, esz);
+    if (r.p) {
+        const Digest e = digest_mem(r.p, r.p_off, r.n, r.p_stride, esz);
+        d.a = fmix(d.a ^ e.a);
+        d.b = fmix(d.b ^ e.b) + 1;
+    }
+    return d;
+}
+
+// Relation r into device buffer dst (keys, then int64 payloads: given or
+// row ids); the device source of the join.
+int upload_rel(hj_ctx *c, int layout, const HostRel &r, void *dst, hj::SrcDev *src) {
     hipStream_t st = c->host_stream;
-    int64_t cap = ns > 0 ? ns : 1;   // optimistic: a key join usually yields <= |S| rows
+    if (layout == kNarrow) {
+        HJ_TRY(upload<int32_t>(dst, (const int32_t *)r.k, r.k_off, r.n, r.k_stride, st));
+        *src = src_col32((const int32_t *)dst, r.n, 0);
+        return HJ_OK;
+    }
+    void *dp = (char *)dst + 8 * (size_t)r.n;
+    HJ_TRY(upload<int64_t>(dst, (const int64_t *)r.k, r.k_off, r.n, r.k_stride, st));
+    if (r.p) {
+        HJ_TRY(upload<int64_t>(dp, (const int64_t *)r.p, r.p_off, r.n, r.p_stride, st));
+    } else if (r.n > 0) {
+        std::vector<int64_t> iota((size_t)r.n);
+        for (int64_t i = 0; i < r.n; ++i) iota[(size_t)i] = i;
+        HJ_TRY(upload<int64_t>(dp, iota.data(), 0, r.n, 1, st));
+    }
+    *src = src_cols64((const int64_t *)dst, (const int64_t *)dp, r.n);
+    return HJ_OK;
+}
+
+// Probe into dbuf[2] / dbuf[3] sized optimistically (|S| rows, or the known
+// M), once more at the exact M when that was too small; *m = M.
+int host_probe_all(hj_ctx *c, int layout, const hj::SrcDev &probe, size_t esz, int64_t guess, int64_t *m) {
+    hipStream_t st = c->host_stream;
+    int64_t cap = guess > 0 ? guess : 1;
     uint64_t cnt = 0;
     for (int pass = 0; pass < 2; ++pass) {
         void *o_r, *o_s;
@@ -693,98 +762,89 @@ int host_probe_all(hj_ctx *c, int layout, const hj::SrcDev &probe, size_t esz, i
     return HJ_OK;
 }
 
-// Full host-memref join, i32 reference types (narrow table).  Result rows go
-// to the device buffers dbuf[2], dbuf[3]; *m receives M.  count_only and the
-// probe call do the same work: the count call's pairs are kept for the probe
-// call that follows it on the same inputs (Memo), as the reference's
-// @countRows leaves its table for @probeRelation.
-int host_join_i32(hj_ctx *c, const int32_t *r, int64_t r_off, int64_t nr, int64_t r_stride,
-                  const int32_t *s, int64_t s_off, int64_t ns, int64_t s_stride, bool /*count_only*/,
-                  int64_t *m, void **d_or, void **d_os) {
-    if (nr < 0 || ns < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
+// Joins a std::thread on every exit path.
+struct Joiner {
+    std::thread t;
+    ~Joiner() {
+        if (t.joinable()) t.join();
+    }
+};
+
+// Host-memref join (the reference's @main data path, join_v2.mlir:627-696).
+//   kHostCount: upload, build, COUNT (no pairs); remember the inputs'
+//               digests (computed while uploading) -- @countRows.
+//   kHostProbe: if both memrefs digest as the last count's, probe the kept
+//               table with the staged probe side into M-row buffers (no
+//               upload, no build) -- @probeRelation; else the whole join.
+//   kHostJoin:  the whole join (one-memref-out C interface), no memo.
+// Pairs land in dbuf[2], dbuf[3] (not for kHostCount); *m = M.
+enum HostMode { kHostCount, kHostProbe, kHostJoin };
+int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMode mode, int64_t *m, void **d_or,
+              void **d_os) {
+    if (r.n < 0 || s.n < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
     HJ_TRY(set_device(c));
     HJ_TRY(host_stream(c));
     hipStream_t st = c->host_stream;
-    const int y = next_set(c);
-    const size_t br = sizeof(int32_t) * (size_t)nr, bs = sizeof(int32_t) * (size_t)ns;
-    void *dr, *ds;
-    HJ_TRY(dbuf(c, 6 + 2 * y, br, &dr));
-    HJ_TRY(dbuf(c, 7 + 2 * y, bs, &ds));
-    HJ_TRY(upload<int32_t>(dr, r, r_off, nr, r_stride, st));
-    HJ_TRY(upload<int32_t>(ds, s, s_off, ns, s_stride, st));
-    bool hit = false;
-    HJ_TRY(memo_hit(c, 32, y, br, bs, &hit));
-    if (!hit) {
-        c->memo.valid = false;
-        HJ_TRY(do_build(c, kNarrow, src_col32((const int32_t *)dr, nr, 0), st));
-        HJ_TRY(host_probe_all(c, kNarrow, src_col32((const int32_t *)ds, ns, 0), sizeof(int32_t), ns, &c->memo.m));
-        c->memo.kind = 32;
-        c->memo.bytes_r = br;
-        c->memo.bytes_s = bs;
-        c->memo.valid = true;
-    } else {
-        ++c->memo_hits;
+    const int esz = layout == kWide ? 8 : 4;
+    hj_ctx::Memo &mm = c->memo;
+    Digest dr, ds;
+    if (mode == kHostProbe && mm.valid && mm.layout == layout && mm.nr == r.n && mm.ns == s.n) {
+        dr = digest_rel(r, esz);
+        ds = digest_rel(s, esz);
+        if (dr == mm.dr && ds == mm.ds) {
+            ++c->memo_hits;
+            const hj::SrcDev src = layout == kWide
+                                       ? src_cols64((const int64_t *)c->dbuf[7], (const int64_t *)c->dbuf[7] + s.n, s.n)
+                                       : src_col32((const int32_t *)c->dbuf[7], s.n, 0);
+            HJ_TRY(host_probe_all(c, layout, src, (size_t)esz, mm.m, m));
+            *d_or = c->dbuf[2];
+            *d_os = c->dbuf[3];
+            return HJ_OK;
+        }
     }
-    c->memo.set = y;
-    *m = c->memo.m;
-    *d_or = c->dbuf[2];
-    *d_os = c->dbuf[3];
+    mm.valid = false;
+    const size_t rb = (size_t)(layout == kWide ? 16 : 4) * (size_t)r.n;
+    const size_t sb = (size_t)(layout == kWide ? 16 : 4) * (size_t)s.n;
+    void *dr_buf, *ds_buf;
+    HJ_TRY(dbuf(c, 6, rb, &dr_buf));
+    HJ_TRY(dbuf(c, 7, sb, &ds_buf));
+    hj::SrcDev rsrc, ssrc;
+    {
+        Joiner dig;
+        if (mode == kHostCount) dig.t = std::thread([&] {   // overlapped with the upload
+            dr = digest_rel(r, esz);
+            ds = digest_rel(s, esz);
+        });
+        HJ_TRY(upload_rel(c, layout, r, dr_buf, &rsrc));
+        HJ_TRY(upload_rel(c, layout, s, ds_buf, &ssrc));
+    }
+    HJ_TRY(do_build(c, layout, rsrc, st));
+    if (mode != kHostCount) {
+        HJ_TRY(host_probe_all(c, layout, ssrc, (size_t)esz, s.n, m));
+        *d_or = c->dbuf[2];
+        *d_os = c->dbuf[3];
+        return HJ_OK;
+    }
+    uint64_t cnt = 0;
+    HJ_TRY(do_probe(c, layout, ssrc, nullptr, nullptr, 0, (uint64_t *)c->dcount, true, st));
+    HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
+    HJ_HIP(hipStreamSynchronize(st));
+    mm.layout = layout;
+    mm.nr = r.n;
+    mm.ns = s.n;
+    mm.dr = dr;
+    mm.ds = ds;
+    mm.m = (int64_t)cnt;
+    mm.valid = true;
+    *m = (int64_t)cnt;
+    *d_or = *d_os = nullptr;
     return HJ_OK;
 }
 
-// Full host-memref join over int64 columns; rpay / spay may be null (payload
-// = row id, as the reference's rowId column, join_v1.mlir:255).  Memoised as
-// host_join_i32.
-int host_join_i64(hj_ctx *c, const int64_t *rk, int64_t rk_off, int64_t rk_stride, const int64_t *rp,
-                  int64_t rp_off, int64_t rp_stride, int64_t nr, const int64_t *sk, int64_t sk_off,
-                  int64_t sk_stride, const int64_t *sp, int64_t sp_off, int64_t sp_stride, int64_t ns,
-                  bool /*count_only*/, int64_t *m, void **d_or, void **d_os) {
-    if (nr < 0 || ns < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
-    HJ_TRY(set_device(c));
-    HJ_TRY(host_stream(c));
-    hipStream_t st = c->host_stream;
-    const int y = next_set(c);
-    const size_t br = 16 * (size_t)nr, bs = 16 * (size_t)ns;   // key column then payload column
-    void *drk, *drp, *dsk, *dsp;
-    HJ_TRY(dbuf(c, 6 + 2 * y, br, &drk));
-    HJ_TRY(dbuf(c, 7 + 2 * y, bs, &dsk));
-    drp = (char *)drk + 8 * (size_t)nr;
-    dsp = (char *)dsk + 8 * (size_t)ns;
-    HJ_TRY(upload<int64_t>(drk, rk, rk_off, nr, rk_stride, st));
-    HJ_TRY(upload<int64_t>(dsk, sk, sk_off, ns, sk_stride, st));
-    if (rp) {
-        HJ_TRY(upload<int64_t>(drp, rp, rp_off, nr, rp_stride, st));
-    } else if (nr > 0) {
-        std::vector<int64_t> iota((size_t)nr);
-        for (int64_t i = 0; i < nr; ++i) iota[(size_t)i] = i;
-        HJ_TRY(upload<int64_t>(drp, iota.data(), 0, nr, 1, st));
-    }
-    if (sp) {
-        HJ_TRY(upload<int64_t>(dsp, sp, sp_off, ns, sp_stride, st));
-    } else if (ns > 0) {
-        std::vector<int64_t> iota((size_t)ns);
-        for (int64_t i = 0; i < ns; ++i) iota[(size_t)i] = i;
-        HJ_TRY(upload<int64_t>(dsp, iota.data(), 0, ns, 1, st));
-    }
-    bool hit = false;
-    HJ_TRY(memo_hit(c, 64, y, br, bs, &hit));
-    if (!hit) {
-        c->memo.valid = false;
-        HJ_TRY(do_build(c, kWide, src_cols64((const int64_t *)drk, (const int64_t *)drp, nr), st));
-        HJ_TRY(host_probe_all(c, kWide, src_cols64((const int64_t *)dsk, (const int64_t *)dsp, ns), sizeof(int64_t), ns,
-                              &c->memo.m));
-        c->memo.kind = 64;
-        c->memo.bytes_r = br;
-        c->memo.bytes_s = bs;
-        c->memo.valid = true;
-    } else {
-        ++c->memo_hits;
-    }
-    c->memo.set = y;
-    *m = c->memo.m;
-    *d_or = c->dbuf[2];
-    *d_os = c->dbuf[3];
-    return HJ_OK;
+HostRel rel32(const int32_t *k, int64_t off, int64_t n, int64_t stride) { return HostRel{k, off, stride, nullptr, 0, 1, n}; }
+HostRel rel64(const int64_t *k, int64_t k_off, int64_t k_stride, const int64_t *p, int64_t p_off, int64_t p_stride,
+              int64_t n) {
+    return HostRel{k, k_off, k_stride, p, p_off, p_stride, n};
 }
 
 // Device column -> strided host memref.
@@ -942,7 +1002,6 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->side) (void)hipFree(c->side);
     if (c->meta) (void)hipFree(c->meta);
     if (c->dcount) (void)hipFree(c->dcount);
-    if (c->join_stats) (void)hipHostFree(c->join_stats);
     for (int i = 0; i < hj_ctx::kDbufs; ++i)
         if (c->dbuf[i]) (void)hipFree(c->dbuf[i]);
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
@@ -999,6 +1058,16 @@ int hj_ctx_build_has_duplicates(hj_ctx *c) {
     HJ_HIP(hipDeviceSynchronize());
     HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
     return v ? 1 : 0;
+}
+
+int hj_ctx_join_kernel(hj_ctx *c) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (!c->join_ran || c->layout < 0) return 0;
+    HJ_TRY(set_device(c));
+    unsigned long long v[2] = {0, 0};
+    HJ_HIP(hipDeviceSynchronize());
+    HJ_HIP(hipMemcpy(v, c->meta + 2, sizeof(v), hipMemcpyDeviceToHost));
+    return hj::join_kernel_choice(c->join_wide, c->join_stream, v[0], v[1]);
 }
 
 int hj_ctx_set_timing(hj_ctx *c, int enable) {
@@ -1201,7 +1270,8 @@ int64_t hj_count_i32(int32_t *, int32_t *r_align, int64_t r_off, int64_t r_size,
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *a, *b;
-    int rc = host_join_i32(c, r_align, r_off, r_size, r_stride, s_align, s_off, s_size, s_stride, true, &m, &a, &b);
+    int rc = host_join(c, kNarrow, rel32(r_align, r_off, r_size, r_stride), rel32(s_align, s_off, s_size, s_stride),
+                       kHostCount, &m, &a, &b);
     return rc == HJ_OK ? m : rc;
 }
 
@@ -1214,8 +1284,8 @@ int32_t hj_probe_i32(int32_t *, int32_t *r_align, int64_t r_off, int64_t r_size,
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
-    HJ_TRY(host_join_i32(c, r_align, r_off, r_size, r_stride, s_align, s_off, s_size, s_stride, false, &m, &d_or,
-                         &d_os));
+    HJ_TRY(host_join(c, kNarrow, rel32(r_align, r_off, r_size, r_stride), rel32(s_align, s_off, s_size, s_stride),
+                     kHostProbe, &m, &d_or, &d_os));
     if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
     HJ_TRY(download<int32_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
     HJ_TRY(download<int32_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));
@@ -1232,8 +1302,8 @@ int64_t hj_count_i64(int64_t *, int64_t *rk, int64_t rk_off, int64_t rk_size, in
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *a, *b;
-    int rc = host_join_i64(c, rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size, sk, sk_off, sk_stride, sp,
-                           sp_off, sp_stride, sk_size, true, &m, &a, &b);
+    int rc = host_join(c, kWide, rel64(rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size),
+                       rel64(sk, sk_off, sk_stride, sp, sp_off, sp_stride, sk_size), kHostCount, &m, &a, &b);
     return rc == HJ_OK ? m : rc;
 }
 
@@ -1249,8 +1319,8 @@ int32_t hj_probe_i64(int64_t *, int64_t *rk, int64_t rk_off, int64_t rk_size, in
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
-    HJ_TRY(host_join_i64(c, rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size, sk, sk_off, sk_stride, sp,
-                         sp_off, sp_stride, sk_size, false, &m, &d_or, &d_os));
+    HJ_TRY(host_join(c, kWide, rel64(rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size),
+                     rel64(sk, sk_off, sk_stride, sp, sp_off, sp_stride, sk_size), kHostProbe, &m, &d_or, &d_os));
     if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
     HJ_TRY(download<int64_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
     HJ_TRY(download<int64_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));
@@ -1270,8 +1340,8 @@ void _mlir_ciface_hj_join_i32(hj_memref2_i32 *res, hj_memref1_i32 *r, hj_memref1
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
-    if (host_join_i32(c, r->aligned, r->offset, r->sizes[0], r->strides[0], s->aligned, s->offset, s->sizes[0],
-                      s->strides[0], false, &m, &d_or, &d_os) != HJ_OK)
+    if (host_join(c, kNarrow, rel32(r->aligned, r->offset, r->sizes[0], r->strides[0]),
+                  rel32(s->aligned, s->offset, s->sizes[0], s->strides[0]), kHostJoin, &m, &d_or, &d_os) != HJ_OK)
         return;
     fill_result<int32_t>(res, d_or, d_os, m, c->host_stream);
 }
@@ -1288,8 +1358,9 @@ void _mlir_ciface_hj_join_i64(hj_memref2_i64 *res, hj_memref1_i64 *r, hj_memref1
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
-    if (host_join_i64(c, r->aligned, r->offset, r->strides[0], nullptr, 0, 1, r->sizes[0], s->aligned, s->offset,
-                      s->strides[0], nullptr, 0, 1, s->sizes[0], false, &m, &d_or, &d_os) != HJ_OK)
+    if (host_join(c, kWide, rel64(r->aligned, r->offset, r->strides[0], nullptr, 0, 1, r->sizes[0]),
+                  rel64(s->aligned, s->offset, s->strides[0], nullptr, 0, 1, s->sizes[0]), kHostJoin, &m, &d_or,
+                  &d_os) != HJ_OK)
         return;
     fill_result<int64_t>(res, d_or, d_os, m, c->host_stream);
 }
@@ -1307,9 +1378,10 @@ void _mlir_ciface_hj_join_kp_i64(hj_memref2_i64 *res, hj_memref1_i64 *rk, hj_mem
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
-    if (host_join_i64(c, rk->aligned, rk->offset, rk->strides[0], rp->aligned, rp->offset, rp->strides[0],
-                      rk->sizes[0], sk->aligned, sk->offset, sk->strides[0], sp->aligned, sp->offset,
-                      sp->strides[0], sk->sizes[0], false, &m, &d_or, &d_os) != HJ_OK)
+    if (host_join(c, kWide, rel64(rk->aligned, rk->offset, rk->strides[0], rp->aligned, rp->offset, rp->strides[0],
+                                  rk->sizes[0]),
+                  rel64(sk->aligned, sk->offset, sk->strides[0], sp->aligned, sp->offset, sp->strides[0], sk->sizes[0]),
+                  kHostJoin, &m, &d_or, &d_os) != HJ_OK)
         return;
     fill_result<int64_t>(res, d_or, d_os, m, c->host_stream);
 }

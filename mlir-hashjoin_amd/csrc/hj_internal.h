@@ -181,18 +181,22 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
                            const BucketSet &out, hipStream_t st);
 size_t radix_item_desc_bytes();
 // work_start: >= radix_work_words words; desc: >= radix_join_items * radix_item_desc_bytes()
-// join_stats (host-mapped, 2 words, may be null): the join leaves there
-// {items deferred by the fast path, items}; general = skip the fast path
-// (k_join over every item), chosen by the caller when the last join on the
-// context deferred most of its items; stream = the probe side is many times
-// the build side (C2): the fast path's larger-sub-chunk shape; bucketed =
-// int64 rows may take k_join_b (the caller passes false after a join whose
-// build keys repeated: join_stats[2], written by k_join_b).
+// sample: the build side's {rows, repeats} from radix_sample (device memory,
+// may be null = "unique"); stream = the probe side is many times the build
+// side (C2): int64 rows take the larger-sub-chunk shape.  The kernel that
+// joins follows from (wide, stream, sample) alone: join_kernel_choice.
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats = nullptr, bool general = false, bool stream = false,
-                      bool bucketed = true);
+                      const unsigned long long *sample, bool stream);
+// After R's partition: sample up to 64 build partitions for repeated keys,
+// adding {rows sampled, rows whose key repeated} into sample[0..1] (zeroed by
+// the caller).  Deterministic for given data.
+hipError_t radix_sample(bool wide, const RadixPlan &pl, const BucketSet &r, unsigned long long *sample,
+                        hipStream_t st);
+// HJ_JOIN_KERNEL_* of the radix join for this shape and sample (host mirror
+// of the device-side choice)
+int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned long long repeats);
 
 // Routing fan-out limit: k_part_scatter (> 512 parts) keeps 12 B of LDS
 // counters per part, k_part_hist 4 B (<= 96 KiB of the 160 KiB).
@@ -200,9 +204,6 @@ constexpr int kMaxRouteParts = 8192;
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
                             hipStream_t st);
-
-// *neq |= 1 when the `bytes` (a multiple of 4) at a and b differ
-hipError_t launch_memeq(const void *a, const void *b, size_t bytes, unsigned long long *neq, hipStream_t st);
 
 // exclusive scan of a u64 array in place (hj_radix.hip); sums >= exclusive_scan_sums(len)
 hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,

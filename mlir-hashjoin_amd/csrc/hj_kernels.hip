@@ -945,32 +945,6 @@ size_t probe_tiles_xcd(unsigned long long max_runs) {
     return (size_t)(max_runs / kXcdTileRuns) + kXcdGroups + 1;
 }
 
-// *neq |= 1 when two device byte ranges differ (host-memref count -> probe reuse)
-__global__ __launch_bounds__(256) void k_memeq(const unsigned *a, const unsigned *b, unsigned long long n,
-                                               unsigned long long *neq) {
-    bool diff = false;
-    const unsigned long long n4 = n / 4;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (unsigned long long)gridDim.x * 256) {
-        const uint4 x = ((const uint4 *)a)[i], y = ((const uint4 *)b)[i];
-        diff |= x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w;
-    }
-    for (unsigned long long i = n4 * 4 + (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (unsigned long long)gridDim.x * 256)
-        diff |= a[i] != b[i];
-    if (__syncthreads_or(diff ? 1 : 0) && threadIdx.x == 0) atomicOr(neq, 1ull);
-}
-
-hipError_t launch_memeq(const void *a, const void *b, size_t bytes, unsigned long long *neq, hipStream_t st) {
-    if (bytes % 4 != 0) return hipErrorInvalidValue;
-    const unsigned long long n = bytes / 4;
-    if (n == 0) return hipSuccess;
-    // uint4 loads need 16-B alignment of both (hipMalloc'd staging buffers are)
-    if ((((uintptr_t)a) | ((uintptr_t)b)) & 15) return hipErrorInvalidValue;
-    const unsigned long long blocks = (n / 4 + 255) / 256;
-    const unsigned g = (unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096);
-    hipLaunchKernelGGL(k_memeq, dim3(g), dim3(256), 0, st, (const unsigned *)a, (const unsigned *)b, n, neq);
-    return hipGetLastError();
-}
-
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
                         bool count_only, unsigned *slow, size_t slow_cap, hipStream_t st) {
     if (src.n <= 0) return hipSuccess;

@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "hj.h"
 #include "hj_internal.h"
 
 namespace hj {
@@ -848,9 +849,78 @@ struct JoinArgs {
     // mode (list != nullptr) joins exactly those items
     unsigned *defer = nullptr, *defer_n = nullptr;
     const unsigned *list = nullptr, *list_n = nullptr;
-    unsigned *stats = nullptr;       // list mode: {deferred items, items} for the caller's next choice
-    unsigned *rep = nullptr;         // k_join_b: set to 1 (host-mapped) when its build keys repeat
+    // build-time sample of the build side (k_rsample): {rows, rows whose key
+    // repeated}; modes: bit m = this launch runs when sample_mode() == m
+    const u64 *sample = nullptr;
+    unsigned modes = 7u;
 };
+
+constexpr unsigned kModeUnique = 1u, kModeSome = 2u, kModeMostlyRepeated = 4u;
+constexpr unsigned kModesAll = kModeUnique | kModeSome | kModeMostlyRepeated;
+constexpr int kSampleParts = 64;   // build partitions sampled (one workgroup each)
+
+// Scalar (s_load) reads of wave-uniform words that no kernel writes while
+// the join runs: through the constant address space.  Plain pointers here
+// compile to vector loads whose results the allocator spilled, and each
+// spill's vmcnt(0) then waited for every row load in flight.
+typedef __attribute__((address_space(4))) const u64 cu64_t;
+__device__ __forceinline__ u64 sload(const u64 *p) { return *(cu64_t *)p; }
+
+// 0: build keys (sampled) unique, 1: some repeat (>= 1/64 of the sampled
+// rows: C1-ref's uniform keys, ~3 %), 2: most repeat (> 1/4: REF-A's ~100
+// copies per key).  Deterministic: a function of exact counts.
+__host__ __device__ __forceinline__ int sample_mode(u64 rows, u64 repeats) {
+    return repeats * 4 > rows ? 2 : (repeats * 64 >= rows && repeats ? 1 : 0);
+}
+__device__ __forceinline__ bool join_runs(const JoinArgs &a) {
+    const int m = a.sample ? sample_mode(sload(a.sample), sload(a.sample + 1)) : 0;
+    return (a.modes >> m) & 1u;
+}
+
+// Build-side sample, launched after R's partition (radix_sample): workgroup
+// i takes partition i * P / nsamp, inserts up to kCap of its keys into an LDS
+// set and counts the rows whose key was already there.  sample[0] += rows
+// inserted, sample[1] += repeats (sample zeroed by the caller).
+template <bool WIDE>
+__global__ __launch_bounds__(1024) void k_rsample(const void *rows, const u64 *runs, const u64 *rstart, int P,
+                                                  unsigned nsamp, u64 *sample) {
+    constexpr int TS = 8192;
+    constexpr unsigned kCap = TS / 2;
+    constexpr u64 kE = ~0ull;   // (a wide key of all ones is skipped: not sampled)
+    __shared__ u64 set[TS];
+    __shared__ unsigned s_n, s_rep;
+    const int p = (int)(((u64)blockIdx.x * (u64)P) / nsamp);
+    for (int j = threadIdx.x; j < TS; j += 1024) set[j] = kE;
+    if (threadIdx.x == 0) s_n = s_rep = 0u;
+    __syncthreads();
+    const u64 lo = rstart[p], hi = rstart[p + 1];
+    const unsigned off = threadIdx.x & 63u;
+    unsigned rep = 0;
+    for (u64 li = lo + (threadIdx.x >> 6); li < hi; li += 16) {
+        const u64 e = runs[li];
+        if (off >= (unsigned)(e & 127u)) continue;
+        const u64 row = (e >> 7) + off;
+        const u64 key = WIDE ? ((const ulonglong2 *)rows)[row].x : (((const u64 *)rows)[row] >> 32);
+        if (key == kE || atomicAdd(&s_n, 1u) >= kCap) continue;
+        unsigned h = (unsigned)((key * 0xD6E8FEB86659FD93ull) >> 51);
+        while (true) {
+            const u64 old = atomicCAS(&set[h], kE, key);
+            if (old == kE) break;
+            if (old == key) {
+                ++rep;
+                break;
+            }
+            h = (h + 1u) & (TS - 1u);
+        }
+    }
+    if (rep) atomicAdd(&s_rep, rep);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned n = s_n < kCap ? s_n : kCap;
+        if (n) atomicAdd(sample, (u64)n);
+        if (s_rep) atomicAdd(sample + 1, (u64)s_rep);
+    }
+}
 
 struct ItemDesc {
     u64 s_lo, s_hi, r_lo, r_hi;      // run positions of the item's S chunk / the partition's R
@@ -886,10 +956,9 @@ __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, c
 // 16 probe reads the first slot only.
 // WPS: minimum waves per SIMD (4: <= 128 VGPRs, 2 workgroups of 512 per CU;
 // 2: <= 256 VGPRs).  RCAPX: build rows per round (0: 5/8 of the slots).
-// PF: prefetch the next item's first R round and S sub-chunk into registers
-// while this item is probed (needs the register room of WPS = 2).
+// LIST: the items of a.list (what the fast kernels deferred) instead of all.
 template <bool WIDE, bool WRITE, int TSL, int NT, int ABL = 0, int SI_ = kJoinItems, int WPS = 4, int RCAPX = 0,
-          bool PF = false, bool LIST = false>
+          bool LIST = false>
 __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -916,10 +985,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     __shared__ unsigned s_cw[SI * NW];        // per (row slot, wave) match counts, then offsets
 
     const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
-    if (LIST && a.stats && blockIdx.x == 0 && threadIdx.x == 0) {
-        a.stats[0] = total;
-        a.stats[1] = a.work_start[a.P];
-    }
     unsigned w = blockIdx.x;
     if (w >= total) return;
     const T *rrows = (const T *)a.r;
@@ -975,24 +1040,14 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
         ents(a.s_runs, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
         return rows_of(srows, es, sv_, SI);
     };
-    T nsv_[PF ? SI : 1];
-    unsigned nsok = 0;
-    bool have_next = false;   // PF: this item's first R round / S sub-chunk already in registers
     while (true) {
         // this item's first R round and first S sub-chunk: issued before the
         // table init so their latency hides behind it.  (Prefetching the next
         // item's R rows instead costs VGPRs -> spills at 4 waves per SIMD, and
-        // measured slower: profiles/r01_micro_join_buckets.txt; PF does it at
-        // 2 waves per SIMD.)
-        if (!have_next) {
-            rok = rows_of(rrows, er, rv_, RI);
-            sok = rows_of(srows, es, sv_, SI);
-        } else if constexpr (PF) {
-#pragma unroll
-            for (int i = 0; i < SI; ++i) sv_[i] = nsv_[i];
-            sok = nsok;
-        }
-        have_next = false;
+        // measured slower: profiles/r01_micro_join_buckets.txt,
+        // profiles/r02_join_prefetch.txt.)
+        rok = rows_of(rrows, er, rv_, RI);
+        sok = rows_of(srows, es, sv_, SI);
         const bool more = w + gridDim.x < total;
         u64 ner[RI], nes[SI];
         ItemDesc nnx = nx;
@@ -1046,14 +1101,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
             if (dup) s_dup = 1u;
             __syncthreads();
             const bool unique = s_dup == 0u;
-            if constexpr (PF) {
-                // the build's rows are dead: the next item's first R round
-                // flies while this item is probed
-                if (more && r0 + rb >= it.r_hi) {
-                    rok = rows_of(rrows, ner, rv_, RI);
-                    have_next = true;
-                }
-            }
             // once per workgroup: every table with a repeated key storing to
             // the one flag serialised those stores at the memory side (C1-ref
             // at 2^28: +3.5 ms, micro/join_micro.hip mode 1)
@@ -1063,31 +1110,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
             }
 
             // ---- probe the chunk, one sub-chunk of S rows at a time
-            bool have_sub = false;   // PF: this sub-chunk's rows are already in nsv_
             for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
-                if (sb != it.s_lo || r0 != it.r_lo) {
-                    if (PF && have_sub) {
-#pragma unroll
-                        for (int i = 0; i < SI; ++i) sv_[i] = nsv_[i];
-                        sok = nsok;
-                    } else {
-                        sok = load_s(sb);
-                    }
-                }
-                have_sub = false;
-                if constexpr (PF) {
-                    // the next sub-chunk of this round (many-sub-chunk items:
-                    // C2) or, after the last one, the next item's first
-                    // sub-chunk flies while this one is probed and written
-                    if (sb + subb < it.s_hi) {
-                        u64 e2[SI];
-                        ents(a.s_runs, sb + subb, sb + 2 * subb < it.s_hi ? sb + 2 * subb : it.s_hi, e2, SI);
-                        nsok = rows_of(srows, e2, nsv_, SI);
-                        have_sub = true;
-                    } else if (have_next) {
-                        nsok = rows_of(srows, nes, nsv_, SI);
-                    }
-                }
+                if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
                 // first slot of every row read before any is resolved (SI
                 // independent LDS reads in flight); most rows end there
                 unsigned m[SI], hp[SI];
@@ -1404,12 +1428,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
 // Run entries, table, duplicate-free probe walk, ballot-compacted output
 // and the ONE cursor atomic per sub-chunk are as in k_join; a partition
 // with a repeated build key (GEN) takes a plain per-row walk to EMPTY.
-// Scalar (s_load) reads of wave-uniform words that no kernel writes while
-// the join runs: through the constant address space.  Plain pointers here
-// compile to vector loads whose results the allocator spilled, and each
-// spill's vmcnt(0) then waited for every row load in flight.
-typedef __attribute__((address_space(4))) const u64 cu64_t;
-__device__ __forceinline__ u64 sload(const u64 *p) { return *(cu64_t *)p; }
 __device__ __forceinline__ ItemDesc sload(const ItemDesc *p) {
     const u64 *q = (const u64 *)p;
     return ItemDesc{sload(q), sload(q + 1), sload(q + 2), sload(q + 3)};
@@ -1451,7 +1469,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
     unsigned w = blockIdx.x;
-    if (w >= total) return;
+    if (w >= total || !join_runs(a)) return;
     const T *rrows = (const T *)a.r;
     const T *srows = (const T *)a.s;
     PT *orr = (PT *)a.out_r;
@@ -1797,7 +1815,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
     unsigned w = blockIdx.x;
-    if (w >= total) return;
+    if (w >= total || !join_runs(a)) return;
     const T *rrows = (const T *)a.r;
     const T *srows = (const T *)a.s;
     PT *orr = (PT *)a.out_r;
@@ -2093,7 +2111,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                             if (!dup_sent) {   // once per workgroup (k_join)
                                 if (threadIdx.x == 0) {
                     __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (a.rep) __hip_atomic_store(a.rep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
                                 dup_sent = true;
                             }
@@ -2143,7 +2160,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             // (early items: the repeat flag, once per workgroup)
             if (threadIdx.x == 0 && early && !dup_sent && s_dup != 0u) {
                 __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (a.rep) __hip_atomic_store(a.rep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 dup_sent = true;
             }
         }
@@ -2177,7 +2193,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
 // 0.65 ms of CAS walks) and the probe scanned the mixed cluster 64 slots per
 // step (profiles/r02_refa_join_ablation.txt).  Items of more than 63 runs
 // (> TS - 64 build rows) go to a.defer (k_join's rounds take them).  LIST: the items of a.list
-// (k_join_u's deferrals), with {items listed, items} into a.stats as k_join.
+// (k_join_u's deferrals) instead of all.
 template <bool WRITE, int NT, int RI, int SI, bool LIST>
 __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     constexpr int TSL = 12, TS = 1 << TSL;
@@ -2198,17 +2214,13 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     __shared__ u64 s_base;
     __shared__ unsigned s_rep;
     const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
-    if (LIST && a.stats && blockIdx.x == 0 && threadIdx.x == 0) {
-        a.stats[0] = total;
-        a.stats[1] = a.work_start[a.P];
-    }
+    if (!join_runs(a)) return;
     const u64 *rrows = (const u64 *)a.r;
     const u64 *srows = (const u64 *)a.s;
     unsigned *orr = (unsigned *)a.out_r;
     unsigned *oss = (unsigned *)a.out_s;
     const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
     const unsigned lane = threadIdx.x & 63u;
-    const u64 lt = lane ? (~0ull >> (64u - lane)) : 0ull;
     bool dup_sent = false;
     auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
 #pragma unroll
@@ -2382,359 +2394,23 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     }
 }
 
-// --------------------------------------------------------------- bucketized join
-// k_join2: the same work items as k_join, but the partition's LDS table is
-// BUCKETIZED and holds no keys:
-//
-//   trow[RCAP]   the round's build rows, row j at index j (16 B wide / 8 B narrow)
-//   tslot[NB]    NB buckets of 4 u32 slots (16 B); slot = fp << 16 | j, EMPTY = ~0
-//   bcnt[NB]     bucket fill counters
-//
-// with bucket = the hash bits right below the partition bits and fp = 16
-// other hash bits (0xFFFF mapped to 0xFFFE, so no real slot equals EMPTY).
-// Build: one LDS atomicAdd per row takes a rank in its bucket (a full
-// bucket sends the row on to the next one, rarely); no CAS loops.  Probe:
-// one 16-B read of the home bucket (ds_read_b128), fingerprint compare of
-// its 4 slots, one read of the candidate row to confirm the key and fetch
-// its payload; only when the bucket is full (~2 % at load factor 0.25) does
-// the probe continue into the next bucket.  The linear-probing table of
-// k_join made every wave wait for the longest of its 64 x 5 chains (6.4
-// extra slots on average at load factor 0.5).
-//
-// Any number of matches per probe row is handled: a sub-chunk whose rows
-// match at most once each is written by ballot compaction (the R payload is
-// already in registers from the confirming read); otherwise every thread
-// re-walks its matching rows' buckets and writes the pairs at its prefix.
-// Keys are compared in full, so INT64_MIN needs no side path here.
-// ABL (diagnostics, micro/join_micro.hip): 1 no cursor atomic, 2 no writes,
-// 4 no probe, 8 no build.
-constexpr int kJ2NT = 512;   // threads per workgroup (2 workgroups per CU at 76 KiB of LDS)
-constexpr int kJ2RI = 5;     // build rows per thread per round: RCAP 2560 (a 2^28-row C3 partition peaks near 2350)
-constexpr int kJ2NBL = 11;   // 2048 buckets x 4 slots: load factor 0.25 at 2048 rows (a full bucket is rare)
-constexpr int kJ2SI = 3;     // S rows per thread per sub-chunk (5 spills: 10.1 ms; 3: 4.96 ms; 2: 4.42 ms)
-template <bool WIDE, bool WRITE, int NT, int RI, int NBL, int SI, int ABL = 0>
-__global__ __launch_bounds__(NT, 4) void k_join2(JoinArgs a) {
-    typedef Row<WIDE> R;
-    typedef typename R::T T;
-    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // output element
-    constexpr int NB = 1 << NBL;
-    constexpr unsigned kBMask = NB - 1;
-    constexpr int RCAP = NT * RI;                 // build rows per round
-    constexpr int SUBR = NT * SI;                 // probe rows per sub-chunk
-    constexpr unsigned rb = (unsigned)RCAP >> kRunLog;
-    constexpr unsigned subb = (unsigned)SUBR >> kRunLog;
-    constexpr unsigned chb = (unsigned)kJoinSub * subb;
-    static_assert((rb << kRunLog) == RCAP && (subb << kRunLog) == SUBR, "rounds must be whole runs");
-    static_assert(RCAP < 4 * NB && RCAP < 0xFFFF, "round must fit the slots and the 16-bit row index");
-    constexpr unsigned kE = 0xFFFFFFFFu;          // EMPTY slot
-    constexpr int NW = NT / 64;
-    __shared__ T trow[RCAP];
-    __shared__ uint4 tslot[NB];                   // bucket b = 4 slots
-    __shared__ unsigned bcnt[NB / 2];             // bucket b's fill in the 16-bit half b & 1 (<= RCAP: no carry)
-    __shared__ u64 wsum[16];
-    __shared__ u64 s_base;
-    __shared__ unsigned s_cw[SI * NW];
-
-    const unsigned total = a.work_start[a.P];
-    unsigned w = blockIdx.x;
-    if (w >= total) return;
-    const T *rrows = (const T *)a.r;
-    const T *srows = (const T *)a.s;
-    PT *orr = (PT *)a.out_r;
-    PT *oss = (PT *)a.out_s;
-    const int tshift = a.tshift;
-    // rank of one more row in bucket b
-    auto take = [&](unsigned b) -> unsigned {
-        return (atomicAdd(&bcnt[b >> 1], (b & 1u) ? 0x10000u : 1u) >> ((b & 1u) * 16u)) & 0xFFFFu;
-    };
-    auto bucket_of = [&](u64 h) -> unsigned { return (unsigned)(h >> tshift) & kBMask; };
-    auto fp_of = [&](u64 h) -> unsigned {
-        const unsigned f = (unsigned)(h >> 16) & 0xFFFFu;
-        return f == 0xFFFFu ? 0xFFFEu : f;
-    };
-    // candidate slots of bucket q for fingerprint f (bit j = slot j)
-    auto cands = [&](const uint4 &q, unsigned f) -> unsigned {
-        return ((q.x >> 16) == f ? 1u : 0u) | ((q.y >> 16) == f ? 2u : 0u) | ((q.z >> 16) == f ? 4u : 0u) |
-               ((q.w >> 16) == f ? 8u : 0u);
-    };
-    auto slot_at = [&](const uint4 &q, unsigned j) -> unsigned {
-        return j == 0 ? q.x : (j == 1 ? q.y : (j == 2 ? q.z : q.w));
-    };
-
-    constexpr unsigned G = NT >> kRunLog;
-    const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
-    const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
-    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
-#pragma unroll
-        for (int i = 0; i < n; ++i) {
-            const u64 li = lo + (u64)i * G + wv0;
-            e[i] = li < hi ? list[li] : 0ull;
-        }
-    };
-    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
-        unsigned ok = 0;
-#pragma unroll
-        for (int i = 0; i < n; ++i) {
-            if (off < (unsigned)(e[i] & 127u)) {
-                v[i] = ld_s<kNtJoinLd>(rows + (e[i] >> 7) + off);
-                ok |= 1u << i;
-            } else {
-                v[i] = R::zero();
-            }
-        }
-        return ok;
-    };
-    T sv_[SI], rv_[RI];
-    unsigned rok = 0, sok = 0;
-    u64 er[RI], es[SI];
-    bool dup_sent = false;
-    ItemDesc it = a.desc[w];
-    ents(a.r_runs, it.r_lo, it.r_lo + rb < it.r_hi ? it.r_lo + rb : it.r_hi, er, RI);
-    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
-    ItemDesc nx = a.desc[w + gridDim.x < total ? w + gridDim.x : w];
-    auto load_r = [&](u64 r0) {
-        ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
-        return rows_of(rrows, er, rv_, RI);
-    };
-    auto load_s = [&](u64 s0) {
-        ents(a.s_runs, s0, s0 + subb < it.s_hi ? s0 + subb : it.s_hi, es, SI);
-        return rows_of(srows, es, sv_, SI);
-    };
-    while (true) {
-        rok = rows_of(rrows, er, rv_, RI);
-        sok = rows_of(srows, es, sv_, SI);
-        const bool more = w + gridDim.x < total;
-        u64 ner[RI], nes[SI];
-        ItemDesc nnx = nx;
-        if (more) {
-            ents(a.r_runs, nx.r_lo, nx.r_lo + rb < nx.r_hi ? nx.r_lo + rb : nx.r_hi, ner, RI);
-            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
-            if (w + 2 * gridDim.x < total) nnx = a.desc[w + 2 * gridDim.x];
-        }
-        for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
-            if (r0 != it.r_lo) rok = load_r(r0);   // later rounds (oversized partitions)
-            // ---- init: every slot EMPTY, every counter 0
-            for (int j = threadIdx.x; j < NB; j += NT) tslot[j] = make_uint4(kE, kE, kE, kE);
-            for (int j = threadIdx.x; j < NB / 2; j += NT) bcnt[j] = 0u;
-            __syncthreads();
-            // ---- build: rows into trow, one rank atomic per row (all issued
-            // before any result is used)
-            {
-                unsigned rk[RI], hb[RI];
-#pragma unroll
-                for (int i = 0; i < RI; ++i) {
-                    const bool act = ((rok >> i) & 1u) && (ABL & 8) == 0;
-                    hb[i] = bucket_of(rhash(R::key(rv_[i])));
-                    if (act) trow[i * NT + threadIdx.x] = rv_[i];
-                    rk[i] = act ? take(hb[i]) : kE;
-                }
-#pragma unroll
-                for (int i = 0; i < RI; ++i) {
-                    if (rk[i] == kE) continue;
-                    unsigned b = hb[i], r = rk[i];
-                    while (r >= 4u) {   // full: on to the next bucket
-                        b = (b + 1) & kBMask;
-                        r = take(b);
-                    }
-                    ((unsigned *)tslot)[b * 4 + r] =
-                        (fp_of(rhash(R::key(rv_[i]))) << 16) | (unsigned)(i * NT + threadIdx.x);
-                }
-            }
-            __syncthreads();
-
-            // ---- probe the chunk, one sub-chunk of S rows at a time
-            for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
-                if (sb != it.s_lo || r0 != it.r_lo) sok = load_s(sb);
-                // per row slot: st = count of confirmed build rows << 16 | the
-                // first one's index in trow; bi = the bucket read last
-                unsigned st[SI], bi[SI];
-                unsigned walk = 0u;   // bit i: row slot i's last bucket was full (walk on)
-                {
-                    uint4 q[SI];
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        bi[i] = bucket_of(rhash(R::key(sv_[i])));
-                        q[i] = ((sok >> i) & 1u) && (ABL & 4) == 0 ? tslot[bi[i]] : make_uint4(kE, kE, kE, kE);
-                    }
-                    // first candidate of every row: confirming key reads in flight together
-                    unsigned pk[SI];
-                    u64 mk[SI];
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const unsigned c = cands(q[i], fp_of(rhash(R::key(sv_[i]))));
-                        if (q[i].w != kE) walk |= 1u << i;
-                        const unsigned j = c ? (unsigned)__builtin_ctz(c) : 0u;
-                        pk[i] = c ? ((slot_at(q[i], j) & 0xFFFFu) | ((c & (c - 1u)) << 16)) : kE;
-                        mk[i] = c ? R::key(trow[slot_at(q[i], j) & 0xFFFFu]) : 0ull;
-                    }
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 key = R::key(sv_[i]);
-                        const bool first = pk[i] != kE && mk[i] == key;
-                        st[i] = first ? ((1u << 16) | (pk[i] & 0xFFFFu)) : 0u;
-                        unsigned rest = pk[i] != kE ? pk[i] >> 16 : 0u;
-                        if (rest) {   // fingerprint twins / repeated build keys: rare
-                            const uint4 qq = tslot[bi[i]];   // (re-read: q is dead by now)
-                            while (rest) {
-                                const unsigned j = __builtin_ctz(rest);
-                                rest &= rest - 1u;
-                                const unsigned x = slot_at(qq, j) & 0xFFFFu;
-                                if (R::key(trow[x]) == key) st[i] = st[i] ? st[i] + (1u << 16) : ((1u << 16) | x);
-                            }
-                        }
-                    }
-                }
-                // rows whose bucket was full walk on, all row slots in one
-                // loop (one LDS round trip per step for the whole wave)
-                while (walk) {
-                    uint4 q[SI];
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if ((walk >> i) & 1u) {
-                            bi[i] = (bi[i] + 1) & kBMask;
-                            q[i] = tslot[bi[i]];
-                        }
-                    }
-                    unsigned nw = 0u;
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if (!((walk >> i) & 1u)) continue;
-                        const u64 key = R::key(sv_[i]);
-                        unsigned c = cands(q[i], fp_of(rhash(key)));
-                        while (c) {
-                            const unsigned j = __builtin_ctz(c);
-                            c &= c - 1u;
-                            const unsigned x = slot_at(q[i], j) & 0xFFFFu;
-                            if (R::key(trow[x]) == key) st[i] = st[i] ? st[i] + (1u << 16) : ((1u << 16) | x);
-                        }
-                        if (q[i].w != kE) nw |= 1u << i;
-                    }
-                    walk = nw;
-                }
-                u64 cnt = 0;
-                unsigned maxc = 0;
-#pragma unroll
-                for (int i = 0; i < SI; ++i) {
-                    const unsigned c = st[i] >> 16;
-                    cnt += c;
-                    maxc = c > maxc ? c : maxc;
-                }
-                // one rule for the whole workgroup: ballot path iff no row matched twice
-                const bool multi = __syncthreads_or(maxc > 1u ? 1 : 0) != 0;
-                if (multi && !dup_sent) {
-                    if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    dup_sent = true;
-                }
-                if (WRITE && !multi) {
-                    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-                    const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-                    unsigned lpre[SI];
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 bal = __ballot(st[i] != 0u);
-                        lpre[i] = (unsigned)__popcll(bal & lt);
-                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
-                    }
-                    __syncthreads();
-                    if (wv == 0) {   // exclusive scan of the SI * NW run lengths
-                        constexpr int K = (SI * NW + 63) / 64;
-                        unsigned v[K], sum = 0;
-#pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            const int j = lane * K + k;
-                            v[k] = j < SI * NW ? s_cw[j] : 0u;
-                            sum += v[k];
-                        }
-                        const unsigned x = wave_incl_add(sum);
-                        unsigned run = x - sum;
-#pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            const int j = lane * K + k;
-                            if (j < SI * NW) s_cw[j] = run;
-                            run += v[k];
-                        }
-                        if (lane == 63 && x)
-                            s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, (u64)x);
-                    }
-                    __syncthreads();
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if constexpr ((ABL & 2) != 0) break;
-                        if (!st[i]) continue;
-                        const u64 pos = s_base + s_cw[i * NW + wv] + lpre[i];
-                        if (pos < (u64)a.cap) {
-                            st_s<kNtJoinSt>(orr + pos, (PT)R::pay(trow[st[i] & 0xFFFFu]));
-                            st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
-                        }
-                    }
-                    __syncthreads();   // s_cw / s_base reused by the next sub-chunk
-                    continue;
-                }
-                u64 tot;
-                const u64 pre = block_excl_scan<NT>(cnt, wsum, &tot);
-                if constexpr (!WRITE) {
-                    if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
-                } else if (tot) {
-                    if (threadIdx.x == 0) s_base = (ABL & 1) ? (u64)w * chb << kRunLog : atomicAdd(a.counter, tot);
-                    __syncthreads();
-                    u64 pos = s_base + pre;
-#pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        if constexpr ((ABL & 2) != 0) break;
-                        if (!st[i]) continue;
-                        const u64 key = R::key(sv_[i]);
-                        const PT spay = (PT)R::pay(sv_[i]);
-                        const u64 h = rhash(key);
-                        const unsigned f = fp_of(h);
-                        unsigned b = bucket_of(h);
-                        uint4 q;
-                        do {   // the home bucket, then on while full
-                            q = tslot[b];
-                            unsigned c = cands(q, f);
-                            while (c) {
-                                const unsigned j = __builtin_ctz(c);
-                                c &= c - 1u;
-                                const T rr = trow[slot_at(q, j) & 0xFFFFu];
-                                if (R::key(rr) != key) continue;
-                                if (pos < (u64)a.cap) {
-                                    orr[pos] = (PT)R::pay(rr);
-                                    oss[pos] = spay;
-                                }
-                                ++pos;
-                            }
-                            b = (b + 1) & kBMask;
-                        } while (q.w != kE);
-                    }
-                    __syncthreads();   // s_base reused by the next sub-chunk
-                }
-            }
-            __syncthreads();   // table reused by the next round / item
-        }
-        if (!more) break;
-        w += gridDim.x;
-        it = nx;
-        nx = nnx;
-#pragma unroll
-        for (int i = 0; i < RI; ++i) er[i] = ner[i];
-#pragma unroll
-        for (int i = 0; i < SI; ++i) es[i] = nes[i];
-    }
-}
-
-
-// Join kernel variant.  Default (kind 0): k_join_u, 768 threads, 3 build +
-// 3 probe rows per thread, 6 waves per SIMD, with k_join over the items it
-// defers (profiles/r02_join_fast.txt: C3 k_join 3.50 -> 2.81 ms, C2 12.34 ->
-// 9.45 ms, C1-ref 1.31 -> 0.96 ms); int64 rows in that shape take k_join_b,
-// its bucketed-table form (C3 2.77 -> 2.55 ms; HJ_JOIN_BKT=0: k_join_u).  HJ_JOIN=1 runs k_join alone (HJ_JOIN_TSL
-// 11 | 12 | 13 picks its table), HJ_JOIN=2 the bucketized k_join2, 3 / 4
-// k_join's register-prefetch variants (all measured slower: DESIGN.md 4).
-struct JoinVariant {
-    int tsl;
-    int nt;
-    int kind;   // 0 k_join_u + k_join, 1 k_join, 2 k_join2, 3 / 4 prefetching k_join
-    int si;     // S rows per thread per sub-chunk
-};
+// --------------------------------------------------------------- join shapes
+// One product kernel per (row width, shape), chosen from facts known when
+// the join is launched -- never from an earlier join's statistics:
+//   int64 rows, fast shape: k_join_b (bucketed table) -- or k_join_u when the
+//     build-time sample found repeated build keys (its counting walks lose to
+//     k_join_u's per-row walks there: C1-ref);
+//   int64 rows, probe side >= 8x the build side: k_join_u's stream shape;
+//   i32 rows: k_join_u (fast shape), its deferrals to k_join_grp, or
+//     k_join_grp over every item when the sample says most build keys repeat
+//     (the reference's 10M x 10M keys in [1, 100k]);
+//   whatever those defer: k_join (list mode).
+// The sample (k_rsample, at build time) lives on the device; every kernel of
+// the join reads it and the ones not chosen exit at once, so the choice is a
+// pure function of the data and needs no host round trip.
+// Fast shape: 768 threads, 3 build + 3 probe rows per thread, 6 waves per
+// SIMD (profiles/r02_join_fast.txt: C3 k_join 3.50 -> 2.81 ms, C2 12.34 ->
+// 9.45 ms, C1-ref 1.31 -> 0.96 ms; k_join_b: C3 2.77 -> 2.55 ms).
 constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 // probe sides much larger than the build side (C2: 2^30 x 2^20, ~1000 S rows
 // per R row): many sub-chunks per item, so bigger sub-chunks and more waves
@@ -2743,32 +2419,7 @@ constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
-JoinVariant join_variant() {
-    static int tsl = [] {
-        const char *e = getenv("HJ_JOIN_TSL");
-        const int v = e ? atoi(e) : 12;
-        return (v == 11 || v == 12 || v == 13) ? v : 12;
-    }();
-    static int kind = [] {
-        const char *e = getenv("HJ_JOIN");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 0 && v <= 4) ? v : 0;
-    }();
-    if (kind == 0) return JoinVariant{12, kFastNT, 0, kFastSI};
-    if (kind == 2) return JoinVariant{12, 512, 2, kJ2SI};
-    if (kind == 3) return JoinVariant{13, 512, 3, 5};   // prefetching k_join, 1 workgroup per CU, 8192 slots
-    if (kind == 4) return JoinVariant{12, 512, 4, 3};   // prefetching k_join, 2 workgroups per CU, 3 S rows
-    return JoinVariant{tsl, tsl == 13 ? 1024 : (tsl == 12 ? 512 : 256), 1, kJoinItems};
-}
-
-// wide rows, fast shape: the bucketed table (k_join_b) unless HJ_JOIN_BKT=0
-bool join_bucketed() {
-    static bool on = [] {
-        const char *e = getenv("HJ_JOIN_BKT");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
+constexpr int kTableLog = 12;   // LDS table slots of every join kernel (2^12)
 
 int cu_count() {
     static int n = [] {
@@ -2813,7 +2464,7 @@ void chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, uns
 // ----------------------------------------------------------------- planning
 RadixPlan radix_plan(long long n_build, int force_bits) {
     // average build rows per partition <= half the join kernel's LDS slots
-    const int tsl = join_variant().tsl;
+    const int tsl = kTableLog;
     RadixPlan pl;
     int bits = 1;
     while (bits < 24 && ((unsigned long long)n_build >> bits) > (1ull << (tsl - 1))) ++bits;
@@ -2879,8 +2530,7 @@ hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, uns
 size_t exclusive_scan_sums(unsigned long long len) { return (size_t)(len / kScanBlock + 2); }
 
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs) {
-    const JoinVariant jv = join_variant();
-    const u64 chr = (u64)kJoinSub * (((u64)jv.nt * jv.si) >> kRunLog);
+    const u64 chr = (u64)kJoinSub * (((u64)kFastNT * kFastSI) >> kRunLog);
     return s_runs / chr + (1ull << pl.total_bits) + 2;
 }
 
@@ -2983,35 +2633,31 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      unsigned *join_stats, bool general, bool stream, bool bucketed) {
+                      const unsigned long long *sample, bool stream) {
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
-    const JoinVariant jv = join_variant();
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
-    // persistent grid: as many workgroups as fit at once (LDS-limited)
-    const int per_cu = jv.kind == 0 || jv.kind == 2 || jv.kind == 4 ? 2 : (jv.tsl == 13 ? 1 : (jv.tsl == 12 ? 2 : 4));
-    const unsigned pg = (unsigned)(per_cu * cu_count());
+    // persistent grids: two workgroups per CU (LDS-limited)
+    const unsigned pg = (unsigned)(2 * cu_count());
+    // the probe-heavy stream shape: int64 rows only (i32 rows keep the fast shape)
+    const bool stream_shape = stream && wide;
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
     // long as ~16 items per workgroup remain for balance
-    const bool fast = jv.kind == 0 && !general;
-    const bool stream_shape = fast && stream;
     const unsigned subb = stream_shape ? (unsigned)((kStreamNT * kStreamSI) >> kRunLog)
-                                       : (unsigned)((jv.nt * jv.si) >> kRunLog);
+                                       : (unsigned)((kFastNT * kFastSI) >> kRunLog);
     u64 chb = (u64)kJoinSub * subb;
     const u64 want = (u64)s_runs / (16ull * pg);
     if (want > chb) chb = (want + subb - 1) / subb * subb;
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
-    // fast path: the deferred-item list lives after the work map; narrow rows
-    // (grp): repeated-key items go to k_join_grp, whose own deferrals
-    // (oversized partitions) follow in a second list for k_join
+    // the deferred-item lists live after the work map: the fast kernels'
+    // (for k_join, or for k_join_grp with i32 rows), then k_join_grp's
     unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
     unsigned *defer2_n = defer_n + 1 + radix_join_items(pl, s_runs);
-    const bool grp = !wide && jv.kind == 0 && (fast || general);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc, fast ? defer_n : nullptr, grp ? defer2_n : nullptr);
+                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -3022,141 +2668,84 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.P = P;
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
-    // the hash bits right below the partition bits: LDS slot (k_join) or bucket (k_join2)
-    a.tshift = 64 - pl.total_bits - (jv.kind == 2 ? kJ2NBL : jv.tsl);
+    // the hash bits right below the partition bits: LDS slot / bucket
+    a.tshift = 64 - pl.total_bits - kTableLog;
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;
     a.counter = counter;
     a.dup_flag = dup_flag;
+    a.sample = sample;
+    a.defer = defer_n + 1;
+    a.defer_n = defer_n;
     const unsigned grid = items < pg ? items : pg;
-#define HJ_JOIN(W, WR, TSL, NT) hipLaunchKernelGGL((k_join<W, WR, TSL, NT>), dim3(grid), dim3(NT), 0, st, a)
-#define HJ_JOIN_V(W, WR)                              \
-    do {                                              \
-        if (jv.tsl == 13) HJ_JOIN(W, WR, 13, 1024);   \
-        else if (jv.tsl == 12) HJ_JOIN(W, WR, 12, 512); \
-        else HJ_JOIN(W, WR, 11, 256);                 \
+#define HJ_LAUNCH(K, NT) hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, st, a)
+#define HJ_WR(K_T, K_F, NT)      \
+    do {                         \
+        if (count_only) HJ_LAUNCH(K_F, NT); \
+        else HJ_LAUNCH(K_T, NT); \
     } while (0)
-#define HJ_JOIN2(W, WR) \
-    hipLaunchKernelGGL((k_join2<W, WR, kJ2NT, kJ2RI, kJ2NBL, kJ2SI>), dim3(grid), dim3(kJ2NT), 0, st, a)
-#define HJ_JOINP(W, WR, TSL, SI, WPS)                                                                        \
-    hipLaunchKernelGGL((k_join<W, WR, TSL, 512, 0, SI, WPS, 2560, true>), dim3(grid), dim3(512), 0, st, a)
-#define HJ_JOINU(W, WR)                                                                                    \
-    do {                                                                                                   \
-        bool st_ = false;                                                                                  \
-        if constexpr (W) st_ = stream_shape;   /* (i32 rows: the fast shape only) */                     \
-        if constexpr (W) {                                                                                 \
-            if (st_)                                                                                       \
-                hipLaunchKernelGGL((k_join_u<true, WR, 12, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),   \
-                                   dim3(grid), dim3(kStreamNT), 0, st, a);                                 \
-        }                                                                                                  \
-        if (!st_) {                                                                                        \
-            if (W && bucketed && join_bucketed())                                                          \
-                hipLaunchKernelGGL((k_join_b<true, WR, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),   \
-                                   dim3(kFastNT), 0, st, a);                                               \
-            else                                                                                           \
-                hipLaunchKernelGGL((k_join_u<W, WR, 12, kFastNT, kFastRI, kFastSI, kFastWPS>), dim3(grid),  \
-                                   dim3(kFastNT), 0, st, a);                                               \
-        }                                                                                                  \
-    } while (0)
-#define HJ_JOINGRP(WR, LST) \
-    hipLaunchKernelGGL((k_join_grp<WR, kGrpNT, kGrpRI, kGrpSI, LST>), dim3(grid), dim3(kGrpNT), 0, st, a)
-    if (fast) {
-        a.defer = defer_n + 1;
-        a.defer_n = defer_n;
-        a.rep = join_stats ? join_stats + 2 : nullptr;
-        if (wide) {
-            if (count_only) HJ_JOINU(true, false);
-            else HJ_JOINU(true, true);
+    if (wide) {
+        if (stream_shape) {
+            a.modes = kModesAll;
+            HJ_WR((k_join_u<true, true, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),
+                  (k_join_u<true, false, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), kStreamNT);
         } else {
-            if (count_only) HJ_JOINU(false, false);
-            else HJ_JOINU(false, true);
+            a.modes = kModeUnique;   // k_join_b: build keys sampled unique
+            HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
+                  (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
+            a.modes = kModesAll & ~kModeUnique;   // k_join_u: repeats sampled
+            HJ_WR((k_join_u<true, true, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>),
+                  (k_join_u<true, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
         }
-        // the items it left, by the general kernel (a persistent grid that
-        // exits at once when the list is empty)
+    } else {
+        // i32 rows: k_join_u unless most build keys repeat; k_join_grp takes
+        // its deferrals (list mode) or, for mostly repeated keys, every item
+        a.modes = kModesAll & ~kModeMostlyRepeated;
+        HJ_WR((k_join_u<false, true, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>),
+              (k_join_u<false, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
         a.list = defer_n + 1;
         a.list_n = defer_n;
-        a.stats = join_stats;
-#define HJ_JOINL(W, WR) \
-    hipLaunchKernelGGL((k_join<W, WR, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512), 0, st, a)
-        if (grp) {
-            // narrow rows: the grouped join takes the deferred items (its
-            // {listed, items} steer the next join), k_join what it defers
-            a.defer = defer2_n + 1;
-            a.defer_n = defer2_n;
-            if (count_only) HJ_JOINGRP(false, true);
-            else HJ_JOINGRP(true, true);
-            a.list = defer2_n + 1;
-            a.list_n = defer2_n;
-            a.stats = nullptr;
-        }
-        if (wide) {
-            if (count_only) HJ_JOINL(true, false);
-            else HJ_JOINL(true, true);
-        } else {
-            if (count_only) HJ_JOINL(false, false);
-            else HJ_JOINL(false, true);
-        }
-#undef HJ_JOINL
-        return hipGetLastError();
-    }
-    if (grp) {
-        // narrow rows after a join that deferred most items (repeated keys):
-        // the grouped join over every item, k_join over what it defers; the
-        // steering stats stay those of the last fast join
         a.defer = defer2_n + 1;
         a.defer_n = defer2_n;
-        if (count_only) HJ_JOINGRP(false, false);
-        else HJ_JOINGRP(true, false);
-        a.list = defer2_n + 1;
-        a.list_n = defer2_n;
-        a.stats = nullptr;
-        if (count_only) hipLaunchKernelGGL((k_join<false, false, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid),
-                                           dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((k_join<false, true, 12, 512, 0, kJoinItems, 4, 0, false, true>), dim3(grid), dim3(512),
-                                0, st, a);
-        return hipGetLastError();
+        HJ_WR((k_join_grp<true, kGrpNT, kGrpRI, kGrpSI, true>), (k_join_grp<false, kGrpNT, kGrpRI, kGrpSI, true>), kGrpNT);
+        a.modes = kModeMostlyRepeated;
+        HJ_WR((k_join_grp<true, kGrpNT, kGrpRI, kGrpSI, false>), (k_join_grp<false, kGrpNT, kGrpRI, kGrpSI, false>),
+              kGrpNT);
     }
-    if (jv.kind == 3 || jv.kind == 4) {
-        if (jv.kind == 3) {
-            if (wide) {
-                if (count_only) HJ_JOINP(true, false, 13, 5, 2);
-                else HJ_JOINP(true, true, 13, 5, 2);
-            } else {
-                if (count_only) HJ_JOINP(false, false, 13, 5, 2);
-                else HJ_JOINP(false, true, 13, 5, 2);
-            }
-        } else {
-            if (wide) {
-                if (count_only) HJ_JOINP(true, false, 12, 3, 4);
-                else HJ_JOINP(true, true, 12, 3, 4);
-            } else {
-                if (count_only) HJ_JOINP(false, false, 12, 3, 4);
-                else HJ_JOINP(false, true, 12, 3, 4);
-            }
-        }
-    } else if (jv.kind == 2) {
-        if (wide) {
-            if (count_only) HJ_JOIN2(true, false);
-            else HJ_JOIN2(true, true);
-        } else {
-            if (count_only) HJ_JOIN2(false, false);
-            else HJ_JOIN2(false, true);
-        }
-    } else if (wide) {
-        if (count_only) HJ_JOIN_V(true, false);
-        else HJ_JOIN_V(true, true);
-    } else {
-        if (count_only) HJ_JOIN_V(false, false);
-        else HJ_JOIN_V(false, true);
-    }
-#undef HJ_JOINP
-#undef HJ_JOINGRP
-#undef HJ_JOINU
-#undef HJ_JOIN2
-#undef HJ_JOIN_V
-#undef HJ_JOIN
+    // what the kernels above deferred (INT64_MIN build keys, oversized
+    // partitions, full tables): k_join over that list, a persistent grid that
+    // exits at once when it is empty
+    a.modes = kModesAll;
+    a.list = wide ? defer_n + 1 : defer2_n + 1;
+    a.list_n = wide ? defer_n : defer2_n;
+    if (wide) HJ_WR((k_join<true, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
+                    (k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), 512);
+    else HJ_WR((k_join<false, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
+               (k_join<false, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), 512);
+#undef HJ_WR
+#undef HJ_LAUNCH
     return hipGetLastError();
+}
+
+hipError_t radix_sample(bool wide, const RadixPlan &pl, const BucketSet &r, unsigned long long *sample,
+                        hipStream_t st) {
+    const int P = 1 << pl.total_bits;
+    const unsigned nsamp = (unsigned)(P < kSampleParts ? P : kSampleParts);
+    if (wide) hipLaunchKernelGGL((k_rsample<true>), dim3(nsamp), dim3(1024), 0, st, (const void *)r.rows,
+                                 (const u64 *)r.runs, (const u64 *)r.rstart, P, nsamp, sample);
+    else hipLaunchKernelGGL((k_rsample<false>), dim3(nsamp), dim3(1024), 0, st, (const void *)r.rows,
+                            (const u64 *)r.runs, (const u64 *)r.rstart, P, nsamp, sample);
+    return hipGetLastError();
+}
+
+int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned long long repeats) {
+    const int m = sample_mode(rows, repeats);
+    if (wide) {
+        if (stream) return HJ_JOIN_KERNEL_STREAM;
+        return m == 0 ? HJ_JOIN_KERNEL_BUCKETED : HJ_JOIN_KERNEL_LINEAR;
+    }
+    return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_LINEAR;
 }
 
 }  // namespace hj

@@ -56,6 +56,7 @@ def _load():
         "hj_ctx_table_capacity": (_i64, [_vp]),
         "hj_ctx_radix_plan": (_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "hj_ctx_build_has_duplicates": (_int, [_vp]),
+        "hj_ctx_join_kernel": (_int, [_vp]),
         "hj_ctx_set_timing": (_int, [_vp, _int]),
         "hj_ctx_last_timing": (_int, [_vp, C.POINTER(C.c_float)]),
         "hj_ctx_last_timing_ex": (_int, [_vp, C.POINTER(C.c_float)]),

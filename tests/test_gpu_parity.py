@@ -133,6 +133,17 @@ def test_memref_count_then_probe_reuses_the_join(oracle):
     assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
     assert hashjoin.lib.hj_host_memo_hits() == h0 + 3
     assert oracle.same_multiset(o_r, o_s, *oracle.nested_loop_i64(rk, rp, sk, sp))
+    # inputs changed BETWEEN count and probe (same addresses, same sizes): the
+    # probe's content digest differs, so it joins afresh instead of reusing
+    m4 = MR.count_i64(rk, rp, sk, sp)
+    sp[::7] += 1000                              # payloads only: same M, other pairs
+    rk[3] = rk[4]                                # and a repeated build key
+    exp4 = oracle.nested_loop_i64(rk, rp, sk, sp)
+    o_r = np.empty(len(exp4[0]), np.int64); o_s = np.empty(len(exp4[0]), np.int64)
+    assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 3
+    assert oracle.same_multiset(o_r, o_s, *exp4)
+    assert m4 >= 0
 
 
 def test_memref_concurrent_host_threads(oracle):

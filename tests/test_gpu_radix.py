@@ -297,30 +297,57 @@ def test_radix_i32_grouped_join_counts_capacity_and_repeats(oracle):
         h.close()
 
 
-def test_fast_path_switch_repeated_joins(oracle):
-    """Join-kernel choice across repeated joins on one context: a join whose
-    items the fast path (k_join_u) mostly defers (i32 keys that repeat ~40x,
-    the reference's REF-A shape) makes the following joins run k_join alone,
-    re-checking the fast path every 8th join; a duplicate-free join in
-    between runs the fast path again.  Every join must equal the oracle."""
+def test_join_kernel_choice_is_deterministic(oracle):
+    """The join kernel is a function of the data (row width, probe / build
+    ratio, the build side's sampled repeats), never of an earlier join on the
+    context: interleaved joins of different shapes each get their own kernel,
+    the same join run twice back to back gets the same one, and every result
+    equals the oracle."""
     h = HashJoin(0)
     try:
         h.set_strategy("radix", radix_bits=6)
+        # i32, ~40 copies of every key (REF-A's shape): the grouped join
         rk = oracle.gen_uniform_i64(7, 1, 1, 400, 16000)[0].astype(np.int32)
         sk = oracle.gen_uniform_i64(7, 2, 1, 400, 12000)[0].astype(np.int32)
         exp = oracle.chained_join_i32(rk, sk, H=64)
+        # i64 PK-FK: the bucketed table
         pk_r, pk_p, pk_s, pk_sp = oracle.gen_pkfk_i64(6, 20000, 30000, 0.9)
         exp_pk = oracle.chained_join_i64(pk_r, pk_p, pk_s, pk_sp, H=200)
-        for i in range(18):
-            if i == 9:   # a duplicate-free i64 join in the middle of the run
-                o_r, o_s = h.join(dev(pk_r), dev(pk_p), dev(pk_s), dev(pk_sp))
-                torch.cuda.synchronize()
-                assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp_pk), f"join {i}"
-                continue
-            o_r, o_s = h.join(dev(rk), None, dev(sk), None)
+        # i64, a repeated key in every tenth build row: the linear-probing join
+        dk, dp = oracle.gen_uniform_i64(8, 1, 1, 1 << 40, 20000)
+        dk = dk.copy()
+        dk[::10] = dk[1::10]
+        sk64, sp64 = oracle.gen_uniform_i64(8, 2, 1, 1 << 40, 20000)
+        sk64 = sk64.copy()
+        sk64[:5000] = dk[:5000]
+        exp_d = oracle.chained_join_i64(dk, dp, sk64, sp64, H=200)
+        # i32 unique-ish keys: the fast i32 join
+        uk = oracle.gen_uniform_i64(9, 1, 1, 1 << 30, 20000)[0].astype(np.int32)
+        us = oracle.gen_uniform_i64(9, 2, 1, 1 << 30, 20000)[0].astype(np.int32)
+        us[:4000] = uk[:4000]
+        exp_u = oracle.chained_join_i32(uk, us, H=200)
+
+        def i32(a, b, want):
+            o_r, o_s = h.join(dev(a), None, dev(b), None)
             torch.cuda.synchronize()
             assert oracle.same_multiset(o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64),
-                                        *exp), f"join {i}"
+                                        want[0].astype(np.int64), want[1].astype(np.int64))
+            return h.join_kernel
+
+        def i64(rk_, rp_, sk_, sp_, want):
+            o_r, o_s = h.join(dev(rk_), dev(rp_), dev(sk_), dev(sp_))
+            torch.cuda.synchronize()
+            assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *want)
+            return h.join_kernel
+
+        seq = [("grp", lambda: i32(rk, sk, exp)), ("grp", lambda: i32(rk, sk, exp)),
+               ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)), ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)),
+               ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)), ("u32", lambda: i32(uk, us, exp_u)),
+               ("grp", lambda: i32(rk, sk, exp)), ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)),
+               ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)), ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk))]
+        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_u", "u32": "k_join_u"}
+        for i, (what, fn) in enumerate(seq):
+            assert fn() == want_k[what], f"join {i} ({what})"
     finally:
         h.close()
 
@@ -336,6 +363,7 @@ def test_radix_probe_heavy_stream_shape(hj, oracle, dist):
         sk, sp = oracle.gen_uniform_i64(11, 2, 1, 3000, 90000)
     o = run(hj, rk, rp, sk, sp, 3)
     assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=300))
+    assert hj.join_kernel == "k_join_u_stream"
 
 
 @pytest.mark.parametrize("rows,bits", [(200000, 7), (180000, 6)])
@@ -359,9 +387,10 @@ def test_radix_bucketed_table_repeat_detection(hj, oracle, rows, bits, dups):
 
 
 def test_wide_join_choice_after_repeats(oracle):
-    """A context whose bucketed join (k_join_b) found repeated int64 build
-    keys runs the next joins with k_join_u (re-trying k_join_b every 8th):
-    results and the repeat flag stay exact across the switches."""
+    """int64 joins alternating between build sides with repeated keys (every
+    partition: k_join_u) and unique keys (k_join_b): each join's kernel
+    follows from its own build side, and results and the repeat flag stay
+    exact across the switches."""
     h = HashJoin(0)
     try:
         rk_u, rp_u, sk_u, sp_u = oracle.gen_pkfk_i64(41, 150000, 150000, 0.9)
@@ -375,5 +404,6 @@ def test_wide_join_choice_after_repeats(oracle):
             o = run(h, rk, rp, sk, sp, 6)
             assert oracle.same_multiset(*o, *want), f"join {i}"
             assert h.has_duplicates() == dup, f"join {i}"
+            assert h.join_kernel == ("k_join_u" if dup else "k_join_b"), f"join {i}"
     finally:
         h.close()
