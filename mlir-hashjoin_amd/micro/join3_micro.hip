@@ -124,7 +124,7 @@ int body(int lg) {
         printf("%-40s %7.3f ms  %7.1f GB/s  M=%llu deferred=%u\n", name, ms, (3.0 * n * (W ? 16 : 8)) / ms / 1e6, m, dn);
     };
     run("radix_join (product)", [&] {
-        CK(radix_join(W, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0));
+        CK(radix_join(W, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0, nullptr, false));
     });
     JoinArgs a;
     a.r = rs.rows; a.s = ss.rows; a.r_runs = rs.runs; a.s_runs = ss.runs; a.r_rstart = rs.rstart;

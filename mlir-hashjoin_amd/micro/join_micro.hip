@@ -136,7 +136,7 @@ int main(int argc, char **argv) {
         printf("%-34s %7.3f ms  %7.1f GB/s  M=%llu\n", name, ms, (3.0 * n * 16) / ms / 1e6, m);
     };
     run("radix_join (product)", [&] {
-        CK(radix_join(true, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0));
+        CK(radix_join(true, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)n, cnt, dup, false, 0, nullptr, false));
     });
     // work map of the product call stays in `work`
     JoinArgs a;
@@ -149,16 +149,6 @@ int main(int argc, char **argv) {
         a.tshift = 64 - pl.total_bits - TSL;                                                              \
         hipLaunchKernelGGL((k_join<true, WR, TSL, NT, ABL>), dim3(PER_CU * cus), dim3(NT), 0, 0, a);      \
     })
-#define JP(TSL, NT, PER_CU, SI, WPS, RCAP, PF, NAME)                                                      \
-    run(NAME, [&] {                                                                                       \
-        a.tshift = 64 - pl.total_bits - TSL;                                                              \
-        hipLaunchKernelGGL((k_join<true, true, TSL, NT, 0, SI, WPS, RCAP, PF>), dim3(PER_CU * cus), dim3(NT), 0, 0, a); \
-    })
-    JP(13, 512, 1, 5, 2, 2560, true, "PF 8192 slots, 512 thr, 1/CU");
-    JP(13, 512, 1, 5, 2, 2560, false, "noPF 8192 slots, 512 thr, 1/CU");
-    JP(12, 512, 1, 5, 2, 2560, true, "PF 4096 slots, 512 thr, 1/CU");
-    JP(13, 1024, 1, 3, 4, 3072, true, "PF 8192 slots, 1024 thr, 1/CU");
-    JP(13, 1024, 1, 3, 4, 3072, false, "noPF 8192 slots, 1024 thr, 1/CU");
     J(12, 512, 2, true, 0, "full");
     J(12, 512, 2, false, 0, "count only");
     J(12, 512, 2, true, 1, "no atomic");

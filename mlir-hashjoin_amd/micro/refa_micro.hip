@@ -77,7 +77,12 @@ int main(int argc, char **argv) {
     void *desc = dalloc<char>(radix_join_items(pl, ss.max_runs) * radix_item_desc_bytes());
     unsigned *out_r = dalloc<unsigned>(cap), *out_s = dalloc<unsigned>(cap);
     u64 *cnt = dalloc<u64>(8), *dup = dalloc<u64>(8);
-    unsigned *stats = dalloc<unsigned>(4);
+    // a build-side sample that says "most keys repeat": the grouped join over every item
+    unsigned long long *stats = dalloc<unsigned long long>(2);
+    {
+        const unsigned long long most[2] = {1, 1};
+        CK(hipMemcpy(stats, most, sizeof(most), hipMemcpyHostToDevice));
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -102,15 +107,14 @@ int main(int argc, char **argv) {
     // the general kernel over every item (what the product runs once the
     // fast path has deferred most items)
     CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)cap, cnt, dup, false, 0,
-                  stats, true, false));
+                  stats, false));
     CK(hipDeviceSynchronize());
     run("product general path (k_join_grp)", [&] {
         CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, (long long)cap, cnt, dup, false, 0,
-                      stats, true, false));
+                      stats, false));
     });
     run("product general, count only", [&] {
-        CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, 0, cnt, dup, true, 0, stats, true,
-                      false));
+        CK(radix_join(false, pl, ws, rs, ss, ss.max_runs, work, desc, out_r, out_s, 0, cnt, dup, true, 0, stats, false));
     });
     JoinArgs a;
     a.r = rs.rows; a.s = ss.rows; a.r_runs = rs.runs; a.s_runs = ss.runs; a.r_rstart = rs.rstart;
