@@ -327,7 +327,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         // per partition in LDS at probe time)
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;   // packed partitioned rows
-        c->plan = hj::radix_plan(src.n, c->radix_bits);
+        c->plan = hj::radix_plan(src.n, c->radix_bits, wide);
         HJ_TRY(ensure_radix_scratch(c, c->rset, src.n, esz, c->plan));
         record(c, kEvInit0, st);
         // meta[0] side count, [1] dup flag, [2..3] the build-side sample
@@ -1033,7 +1033,7 @@ int hj_ctx_reserve(hj_ctx *c, int64_t max_build_rows, int key_bits) {
         HJ_TRY(ensure_table(c, max_build_rows, key_bits == 64 ? kWide : kNarrow));
         if (c->strategy != HJ_STRATEGY_AUTO || max_build_rows < kDualMinBuildRows) return HJ_OK;
     }
-    const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits);
+    const hj::RadixPlan pl = hj::radix_plan(max_build_rows, c->radix_bits, key_bits == 64);
     return ensure_radix_scratch(c, c->rset, max_build_rows, esz, pl);
 }
 

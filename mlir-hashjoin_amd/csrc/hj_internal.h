@@ -168,7 +168,8 @@ struct RadixNeed {                 // sizes of one bucket set
     unsigned long long buckets, rows;
 };
 
-RadixPlan radix_plan(long long n_build, int force_bits = 0);   // force_bits > 0: fixed 2^bits partitions
+// force_bits > 0: fixed 2^bits partitions; wide: int64 rows (else i32 rows, twice the rows per partition)
+RadixPlan radix_plan(long long n_build, int force_bits = 0, bool wide = true);
 // Bucket capacity of the final set (`final_set`) or the ping set of plan pl for n rows.
 RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set);
 unsigned long long radix_tiles(long long n, int max_nseg);

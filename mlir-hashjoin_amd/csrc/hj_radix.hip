@@ -1799,7 +1799,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     constexpr unsigned rmax = (unsigned)TS >> kRunLog;
     constexpr unsigned rmax_rows = (unsigned)(TS * 3 / 4);
     static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
-    constexpr unsigned kNone = 0xFFFFFFFFu;
+    constexpr unsigned kNone = 0xFFFFFFFFu, kMulti = 0xFFFFFFFEu;
     __shared__ __attribute__((aligned(16))) u64 tkey[TS];
     __shared__ __attribute__((aligned(16))) u64 tpay[WIDE ? TS : 2];
     __shared__ __attribute__((aligned(16))) unsigned bcnt[NB];
@@ -1809,8 +1809,14 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     __shared__ u64 s_base;
     __shared__ __attribute__((aligned(16))) unsigned s_ctl[4];   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
     unsigned &s_bad = s_ctl[0], &s_dup = s_ctl[1], &s_rows = s_ctl[2], &s_nsus = s_ctl[3];
-    __shared__ unsigned s_cw[SI * NW];
-    __shared__ u64 wsum[16];
+    // slots whose key is held by another live slot too (set by the suspects'
+    // chain checks): a probe row whose first match is marked takes the
+    // multi-match path
+    __shared__ __attribute__((aligned(16))) unsigned sdup[TS / 32];
+    // per (row slot, wave) ballot counts, then per wave the multi rows' pairs
+    __shared__ unsigned s_cw[SI * NW + NW];
+    __shared__ unsigned s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
+    __shared__ unsigned s_mpre[NT];   // a thread's multi pairs before it in its wave (kept out of registers)
     bool dup_sent = false;
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
@@ -1885,9 +1891,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             const uint4 z4 = make_uint4(z, z, z, z);
             // (thread 0 clears the control words: it is also the one that
             // reads the previous item's s_dup after the item's last barrier)
-            static_assert(NB / 2 <= NT, "one 16-B clear per thread: counts, signatures");
-            if (threadIdx.x < NB / 4) ((uint4 *)bcnt)[threadIdx.x] = z4;
-            else if (threadIdx.x < NB / 2) ((uint4 *)bsig)[threadIdx.x - NB / 4] = z4;
+            static_assert(NB / 2 + TS / 128 <= NT, "one 16-B clear per thread: counts, signatures, repeat marks");
+            // (the index carries z too: a loop-invariant clear address was
+            // hoisted out of the item loop and spilled)
+            const unsigned ci = threadIdx.x + z;
+            if (ci < NB / 4) ((uint4 *)bcnt)[ci] = z4;
+            else if (ci < NB / 2) ((uint4 *)bsig)[ci - NB / 4] = z4;
+            else if (ci < NB / 2 + TS / 128) ((uint4 *)sdup)[ci - NB / 2] = z4;
             if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
             __syncthreads();
             // ---- build: every row's rank add issued before any is used
@@ -1950,46 +1960,71 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             }
             if (bad) s_bad = 1u;
             __syncthreads();
-            bool early = false;   // (see below)
             if (s_bad) {
                 if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             } else {
-            // ---- repeated build keys: each suspect looks for another live
-            // slot with its key along its chain (home bucket, then on while a
-            // bucket's count says a row passed it)
-            // Unique build keys leave ~rows^2 / (64 NB) suspects (fingerprint
-            // collisions in a home bucket); clearly more means repeats are
-            // likely, and then the verdict is waited for before the probe
-            // (no unique-path probe thrown away).  Either way it is exact.
-            const unsigned nsus = s_nsus, nrows = s_rows;
-            early = (u64)nsus * (64u * NB) * 2u > 3ull * nrows * nrows;
+            // ---- repeated build keys: each suspect walks its chain (home
+            // bucket, then on while a bucket's count says a row passed it) and,
+            // when another live slot holds its key, marks EVERY live slot with
+            // that key, itself included.  Of c copies of a key all but the
+            // first to OR its fingerprint are suspects, so every copy gets
+            // marked.  The verdict (s_dup) is read after the first sub-chunk's
+            // ballot barrier: the walks overlap the probe's reads.
             {
                 unsigned ndup = 0;
+                const unsigned nsus = s_nsus;
                 for (unsigned q = threadIdx.x; q < nsus && !(ABL & 1); q += NT) {
                     const unsigned e = sus[q], slot = e & 0xFFFFu;
-                    unsigned h = e >> 16;
                     const u64 key = kof(tkey[slot]);
-                    bool d = false;
+                    unsigned h = e >> 16;
+                    bool twin = false;
+                    // one walk: every other live slot with the key is marked as
+                    // found, the suspect's own slot after the walk if any was
                     for (unsigned g = 0; g < (unsigned)NB; ++g) {
                         unsigned c;
                         u64 k4[BW];
                         read_bucket(h, c, k4);
 #pragma unroll
-                        for (int j = 0; j < BW; ++j)
-                            d |= (unsigned)j < c && h * BW + (unsigned)j != slot && kof(k4[j]) == key;
-                        if (d || c <= (unsigned)BW) break;
+                        for (int j = 0; j < BW; ++j) {
+                            const unsigned sl = h * BW + (unsigned)j;
+                            if ((unsigned)j < c && sl != slot && kof(k4[j]) == key) {
+                                atomicOr(&sdup[sl >> 5], 1u << (sl & 31u));
+                                twin = true;
+                            }
+                        }
+                        if (c <= (unsigned)BW) break;
                         h = (h + 1u) & kBMask;
                     }
-                    ndup += d ? 1u : 0u;
+                    if (twin) {
+                        ++ndup;
+                        atomicOr(&sdup[slot >> 5], 1u << (slot & 31u));
+                    }
                 }
                 if (ndup) atomicAdd(&s_dup, ndup);
             }
-            // (otherwise the suspects' verdict is read after the first
-            // sub-chunk's probe barrier: their walks overlap the probe's reads)
-            // Likely repeats: straight to the counting walks (exact for any
-            // keys); the suspects' verdict then only feeds the repeat flag,
-            // read after the item's last barrier.
-            bool known = early, unique = !early;
+            // the matches of `key` along its chain: counted, or written from pos
+            auto chain = [&](u64 key, bool wr, u64 pos, PT spay) {
+                unsigned h = bucket(key), cnt = 0;
+                for (unsigned g = 0; g < (unsigned)NB; ++g) {
+                    unsigned c;
+                    u64 k4[BW];
+                    read_bucket(h, c, k4);
+#pragma unroll
+                    for (int j = 0; j < BW; ++j) {
+                        if ((unsigned)j < c && kof(k4[j]) == key) {
+                            if (WRITE && wr && pos + cnt < (u64)a.cap) {
+                                orr[pos + cnt] = WIDE ? (PT)tpay[h * BW + j] : (PT)(k4[j] & 0xffffffffull);
+                                oss[pos + cnt] = spay;
+                            }
+                            ++cnt;
+                        }
+                    }
+                    if (c <= (unsigned)BW) break;
+                    h = (h + 1u) & kBMask;
+                }
+                return cnt;
+            };
+            bool known = false, dups = false;
                 for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
                     if (sb != it.s_lo) {
                         ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
@@ -1999,74 +2034,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
 #pragma unroll
                     for (int i = 0; i < SI; ++i)
                         if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64)) pm |= 1u << i;
-                    // repeated build keys: each row counts its matches along
-                    // its chain, then walks it again writing at its prefix;
-                    // true: the item went to k_join (nothing written)
-                    auto gen_sub = [&](u64 sb, unsigned pm) -> bool {
-                        unsigned cnt = 0, mb = 0u;
-#pragma unroll
-                        for (int i = 0; i < SI; ++i) {
-                            if (!((pm >> i) & 1u)) continue;
-                            const u64 key = R::key(sv_[i]);
-                            unsigned h = bucket(key);
-                            const unsigned c0 = cnt;
-                            for (unsigned g = 0; g < (unsigned)NB; ++g) {
-                                unsigned c;
-                                u64 k4[BW];
-                                read_bucket(h, c, k4);
-#pragma unroll
-                                for (int j = 0; j < BW; ++j) cnt += ((unsigned)j < c && kof(k4[j]) == key) ? 1u : 0u;
-                                if (c <= (unsigned)BW) break;
-                                h = (h + 1u) & kBMask;
-                            }
-                            if (cnt != c0) mb |= 1u << i;
-                        }
-                        u64 tot;
-                        const u64 pre = block_excl_scan<NT>((u64)cnt, wsum, &tot);
-                        if (!WIDE && WRITE && sb == it.s_lo && tot > (u64)(2 * NT * SI)) {
-                            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
-                            return true;
-                        }
-                        if constexpr (!WRITE) {
-                            if (threadIdx.x == 0 && tot) atomicAdd(a.counter, tot);
-                        } else if (tot) {
-                            if (threadIdx.x == 0) s_base = atomicAdd(a.counter, tot);
-                            __syncthreads();
-                            u64 pos = s_base + pre;
-#pragma unroll
-                            for (int i = 0; i < SI; ++i) {
-                                if (!((mb >> i) & 1u)) continue;
-                                const u64 key = R::key(sv_[i]);
-                                const PT spay = (PT)R::pay(sv_[i]);
-                                unsigned h = bucket(key);
-                                for (unsigned g = 0; g < (unsigned)NB; ++g) {
-                                    unsigned c;
-                                    u64 k4[BW];
-                                    read_bucket(h, c, k4);
-#pragma unroll
-                                    for (int j = 0; j < BW; ++j) {
-                                        if ((unsigned)j < c && kof(k4[j]) == key) {
-                                            if (pos < (u64)a.cap) {
-                                                orr[pos] = WIDE ? (PT)tpay[h * BW + j] : (PT)(k4[j] & 0xffffffffull);
-                                                oss[pos] = spay;
-                                            }
-                                            ++pos;
-                                        }
-                                    }
-                                    if (c <= (unsigned)BW) break;
-                                    h = (h + 1u) & kBMask;
-                                }
-                            }
-                        }
-                        __syncthreads();
-                        return false;
-                    };
-                    if (known && !unique) {
-                        if (gen_sub(sb, pm)) break;
-                        continue;
-                    }
-                    // unique build keys: the home bucket of every row read
-                    // before any is resolved
+                    // every row's first match: the home buckets of all rows
+                    // read before any is resolved
                     unsigned m[SI], hb[SI], cb[SI];
 #pragma unroll
                     for (int i = 0; i < SI; ++i) {
@@ -2098,70 +2067,103 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         }
                     }
                     const int wv = threadIdx.x >> 6;
+                    // multi rows (first match on a marked slot; m = kMulti): all
+                    // their pairs go out by a chain walk from a wave-prefix
+                    // position; the others by ballot compaction
+                    unsigned cntm = 0u;
+                    auto split = [&]() {
 #pragma unroll
-                    for (int i = 0; i < SI; ++i) {
-                        const u64 bal = __ballot(m[i] != kNone);
-                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
-                    }
+                        for (int i = 0; i < SI; ++i) {
+                            if (m[i] != kNone && ((sdup[m[i] >> 5] >> (m[i] & 31u)) & 1u)) {
+                                m[i] = kMulti;
+                                cntm += chain(R::key(sv_[i]), false, 0, (PT)0);
+                            }
+                        }
+                    };
+                    auto ballots = [&]() {
+#pragma unroll
+                        for (int i = 0; i < SI; ++i) {
+                            const u64 bal = __ballot(m[i] < kMulti);
+                            if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                        }
+                        const unsigned xm = wave_incl_add(cntm);
+                        if (dups) s_mpre[threadIdx.x] = xm - cntm;
+                        if (lane == 63) s_cw[SI * NW + wv] = xm;
+                    };
+                    if (dups) split();
+                    ballots();
                     __syncthreads();
                     if (!known) {
                         known = true;
-                        unique = s_dup == 0u;
-                        if (!unique) {
+                        dups = s_dup != 0u;
+                        if (dups) {
                             if (!dup_sent) {   // once per workgroup (k_join)
-                                if (threadIdx.x == 0) {
-                    __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                                if (threadIdx.x == 0)
+                                    __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 dup_sent = true;
                             }
-                            if (gen_sub(sb, pm)) break;
-                            continue;
+                            split();     // (the marks are complete now)
+                            ballots();   // (s_cw: nothing reads it before this barrier)
+                            __syncthreads();
                         }
                     }
                     if (wv == 0) {
-                        constexpr int K = (SI * NW + 63) / 64;
-                        unsigned v[K], sum = 0;
+                        constexpr int NE = SI * NW + NW;
+                        constexpr int K = (NE + 63) / 64;
+                        unsigned v[K], sum = 0, msum = 0;
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
                             const int jj = lane * K + k;
-                            v[k] = jj < SI * NW ? s_cw[jj] : 0u;
+                            v[k] = jj < NE ? s_cw[jj] : 0u;
                             sum += v[k];
+                            msum += jj >= SI * NW ? v[k] : 0u;
                         }
                         const unsigned x = wave_incl_add(sum);
+                        const unsigned mt = wave_incl_add(msum);
                         unsigned run = x - sum;
 #pragma unroll
                         for (int k = 0; k < K; ++k) {
                             const int jj = lane * K + k;
-                            if (jj < SI * NW) s_cw[jj] = run;
+                            if (jj < NE) s_cw[jj] = run;
                             run += v[k];
                         }
-                        if (lane == 63 && x) {
-                            if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
-                            else atomicAdd(a.counter, (u64)x);
+                        if (lane == 63) {
+                            // i32 rows with many pairs per probe row (the
+                            // reference's keys in [1, 100k]): the item goes to
+                            // k_join_grp before anything of it is written
+                            const bool skip = !WIDE && WRITE && sb == it.s_lo && mt > (unsigned)(2 * NT * SI);
+                            s_skip = skip ? 1u : 0u;
+                            if (skip) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+                            else if (x) {
+                                if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
+                                else atomicAdd(a.counter, (u64)x);
+                            }
                         }
                     }
                     if constexpr (WRITE) {
                         __syncthreads();
+                        if (s_skip) break;
 #pragma unroll
                         for (int i = 0; i < SI; ++i) {
-                            const u64 bal = __ballot(m[i] != kNone);
-                            if (m[i] == kNone) continue;
+                            const u64 bal = __ballot(m[i] < kMulti);
+                            if (m[i] >= kMulti) continue;
                             const u64 pos = s_base + s_cw[i * NW + wv] + (unsigned)__popcll(bal & lt);
                             if (pos < (u64)a.cap) {
                                 st_s<kNtJoinSt>(orr + pos, WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull));
                                 st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
                             }
                         }
+                        if (dups) {
+                            u64 pos = s_base + s_cw[SI * NW + wv] + s_mpre[threadIdx.x];
+#pragma unroll
+                            for (int i = 0; i < SI; ++i)
+                                if (m[i] == kMulti) pos += chain(R::key(sv_[i]), true, pos, (PT)R::pay(sv_[i]));
+                        }
                     }
                     if (sb + subb < it.s_hi) __syncthreads();
                 }
             }
-            __syncthreads();
-            // (early items: the repeat flag, once per workgroup)
-            if (threadIdx.x == 0 && early && !dup_sent && s_dup != 0u) {
-                __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                dup_sent = true;
-            }
+            __syncthreads();   // table reused by the next item
         }
         if (!more) break;
         w += gridDim.x;
@@ -2419,7 +2421,27 @@ constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
-constexpr int kTableLog = 12;   // LDS table slots of every join kernel (2^12)
+constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
+// i32 rows (k_join_u): threads, build / probe rows per thread, waves per
+// SIMD, workgroups per CU, table slots (log2) and the plan's partition size
+// (log2 of twice the average build rows).  HJ_NARROW_SHAPE picks one for
+// experiment builds (make EXTRA=-DHJ_NARROW_SHAPE=n); the product has one.
+#ifndef HJ_NARROW_SHAPE
+#define HJ_NARROW_SHAPE 0
+#endif
+#if HJ_NARROW_SHAPE == 1
+constexpr int kNarrowNT = 512, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 8, kNarrowPerCU = 4, kTableLogNarrow = 12,
+              kPlanLogNarrow = 12;
+#elif HJ_NARROW_SHAPE == 2
+constexpr int kNarrowNT = 512, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 8, kNarrowPerCU = 4, kTableLogNarrow = 12,
+              kPlanLogNarrow = 11;
+#elif HJ_NARROW_SHAPE == 3
+constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 12,
+              kPlanLogNarrow = 12;
+#else
+constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
+              kPlanLogNarrow = 13;
+#endif
 
 int cu_count() {
     static int n = [] {
@@ -2462,9 +2484,9 @@ void chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, uns
 }  // namespace
 
 // ----------------------------------------------------------------- planning
-RadixPlan radix_plan(long long n_build, int force_bits) {
+RadixPlan radix_plan(long long n_build, int force_bits, bool wide) {
     // average build rows per partition <= half the join kernel's LDS slots
-    const int tsl = kTableLog;
+    const int tsl = wide ? kTableLog : kPlanLogNarrow;
     RadixPlan pl;
     int bits = 1;
     while (bits < 24 && ((unsigned long long)n_build >> bits) > (1ull << (tsl - 1))) ++bits;
@@ -2530,7 +2552,10 @@ hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, uns
 size_t exclusive_scan_sums(unsigned long long len) { return (size_t)(len / kScanBlock + 2); }
 
 unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_runs) {
-    const u64 chr = (u64)kJoinSub * (((u64)kFastNT * kFastSI) >> kRunLog);
+    // the smallest item of any shape (radix_join sizes items by its kernel's sub-chunk)
+    const u64 sub = (u64)kFastNT * kFastSI < (u64)kNarrowNT * kNarrowSI ? (u64)kFastNT * kFastSI
+                                                                         : (u64)kNarrowNT * kNarrowSI;
+    const u64 chr = (u64)kJoinSub * (sub >> kRunLog);
     return s_runs / chr + (1ull << pl.total_bits) + 2;
 }
 
@@ -2637,17 +2662,20 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
-    // persistent grids: two workgroups per CU (LDS-limited)
+    // persistent grids: two workgroups per CU (LDS-limited); i32 rows' fast
+    // kernel kNarrowPerCU
     const unsigned pg = (unsigned)(2 * cu_count());
+    const unsigned pgn = (unsigned)(kNarrowPerCU * cu_count());
     // the probe-heavy stream shape: int64 rows only (i32 rows keep the fast shape)
     const bool stream_shape = stream && wide;
     // S runs per work item: at least kJoinSub sub-chunks, more when S is
     // large against the partition count (each item rebuilds its R table), as
     // long as ~16 items per workgroup remain for balance
     const unsigned subb = stream_shape ? (unsigned)((kStreamNT * kStreamSI) >> kRunLog)
-                                       : (unsigned)((kFastNT * kFastSI) >> kRunLog);
+                                       : (wide ? (unsigned)((kFastNT * kFastSI) >> kRunLog)
+                                               : (unsigned)((kNarrowNT * kNarrowSI) >> kRunLog));
     u64 chb = (u64)kJoinSub * subb;
-    const u64 want = (u64)s_runs / (16ull * pg);
+    const u64 want = (u64)s_runs / (16ull * (wide ? pg : pgn));
     if (want > chb) chb = (want + subb - 1) / subb * subb;
     chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
@@ -2669,7 +2697,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
     // the hash bits right below the partition bits: LDS slot / bucket
-    a.tshift = 64 - pl.total_bits - kTableLog;
+    a.tshift = 64 - pl.total_bits - (wide ? kTableLog : kTableLogNarrow);
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;
@@ -2691,19 +2719,31 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             HJ_WR((k_join_u<true, true, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),
                   (k_join_u<true, false, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), kStreamNT);
         } else {
-            a.modes = kModeUnique;   // k_join_b: build keys sampled unique
+            // k_join_b unless most build keys repeat (its multi-match walks
+            // lose to k_join_u's per-row walks there)
+            a.modes = kModeUnique | kModeSome;
             HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
-            a.modes = kModesAll & ~kModeUnique;   // k_join_u: repeats sampled
+            a.modes = kModeMostlyRepeated;
             HJ_WR((k_join_u<true, true, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_u<true, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
         }
     } else {
-        // i32 rows: k_join_u unless most build keys repeat; k_join_grp takes
-        // its deferrals (list mode) or, for mostly repeated keys, every item
-        a.modes = kModesAll & ~kModeMostlyRepeated;
-        HJ_WR((k_join_u<false, true, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>),
-              (k_join_u<false, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
+        // i32 rows: k_join_u over an 8192-slot table (the bucketed table's
+        // count + two 16-B reads per probe row lose to one 8-B slot read for
+        // 8-B rows: REF-B 1.42 vs 1.24 ms) unless most build keys repeat;
+        // k_join_grp takes its deferrals (list mode) or, for mostly repeated
+        // keys, every item
+        a.modes = kModeUnique | kModeSome;
+        {
+            const unsigned gn = items < pgn ? items : pgn;
+            if (count_only)
+                hipLaunchKernelGGL((k_join_u<false, false, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
+                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
+            else
+                hipLaunchKernelGGL((k_join_u<false, true, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
+                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
+        }
         a.list = defer_n + 1;
         a.list_n = defer_n;
         a.defer = defer2_n + 1;
@@ -2743,7 +2783,7 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
     const int m = sample_mode(rows, repeats);
     if (wide) {
         if (stream) return HJ_JOIN_KERNEL_STREAM;
-        return m == 0 ? HJ_JOIN_KERNEL_BUCKETED : HJ_JOIN_KERNEL_LINEAR;
+        return m == 2 ? HJ_JOIN_KERNEL_LINEAR : HJ_JOIN_KERNEL_BUCKETED;
     }
     return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_LINEAR;
 }

@@ -313,7 +313,8 @@ def test_join_kernel_choice_is_deterministic(oracle):
         # i64 PK-FK: the bucketed table
         pk_r, pk_p, pk_s, pk_sp = oracle.gen_pkfk_i64(6, 20000, 30000, 0.9)
         exp_pk = oracle.chained_join_i64(pk_r, pk_p, pk_s, pk_sp, H=200)
-        # i64, a repeated key in every tenth build row: the linear-probing join
+        # i64, a repeated key in every tenth build row: still the bucketed
+        # table (its marked-slot multi-match path)
         dk, dp = oracle.gen_uniform_i64(8, 1, 1, 1 << 40, 20000)
         dk = dk.copy()
         dk[::10] = dk[1::10]
@@ -321,7 +322,11 @@ def test_join_kernel_choice_is_deterministic(oracle):
         sk64 = sk64.copy()
         sk64[:5000] = dk[:5000]
         exp_d = oracle.chained_join_i64(dk, dp, sk64, sp64, H=200)
-        # i32 unique-ish keys: the fast i32 join
+        # i64, keys in [1, 2000] (~90 % of the build rows repeat): k_join_u
+        hk, hp = oracle.gen_uniform_i64(10, 1, 1, 2000, 20000)
+        hs, hsp = oracle.gen_uniform_i64(10, 2, 1, 2000, 6000)
+        exp_h = oracle.chained_join_i64(hk, hp, hs, hsp, H=200)
+        # i32 unique-ish keys: k_join_u (8192-slot table)
         uk = oracle.gen_uniform_i64(9, 1, 1, 1 << 30, 20000)[0].astype(np.int32)
         us = oracle.gen_uniform_i64(9, 2, 1, 1 << 30, 20000)[0].astype(np.int32)
         us[:4000] = uk[:4000]
@@ -344,8 +349,10 @@ def test_join_kernel_choice_is_deterministic(oracle):
                ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)), ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)),
                ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)), ("u32", lambda: i32(uk, us, exp_u)),
                ("grp", lambda: i32(rk, sk, exp)), ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)),
-               ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)), ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk))]
-        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_u", "u32": "k_join_u"}
+               ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)), ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)),
+               ("h", lambda: i64(hk, hp, hs, hsp, exp_h)), ("u32", lambda: i32(uk, us, exp_u)),
+               ("h", lambda: i64(hk, hp, hs, hsp, exp_h))]
+        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_b", "u32": "k_join_u", "h": "k_join_u"}
         for i, (what, fn) in enumerate(seq):
             assert fn() == want_k[what], f"join {i} ({what})"
     finally:
@@ -387,10 +394,9 @@ def test_radix_bucketed_table_repeat_detection(hj, oracle, rows, bits, dups):
 
 
 def test_wide_join_choice_after_repeats(oracle):
-    """int64 joins alternating between build sides with repeated keys (every
-    partition: k_join_u) and unique keys (k_join_b): each join's kernel
-    follows from its own build side, and results and the repeat flag stay
-    exact across the switches."""
+    """int64 joins alternating between build sides with repeated keys in
+    every partition (k_join_b's multi-match path) and unique keys: results
+    and the repeat flag stay exact across the switches."""
     h = HashJoin(0)
     try:
         rk_u, rp_u, sk_u, sp_u = oracle.gen_pkfk_i64(41, 150000, 150000, 0.9)
@@ -404,6 +410,45 @@ def test_wide_join_choice_after_repeats(oracle):
             o = run(h, rk, rp, sk, sp, 6)
             assert oracle.same_multiset(*o, *want), f"join {i}"
             assert h.has_duplicates() == dup, f"join {i}"
-            assert h.join_kernel == ("k_join_u" if dup else "k_join_b"), f"join {i}"
+            assert h.join_kernel == "k_join_b", f"join {i}"
     finally:
         h.close()
+
+
+@pytest.mark.parametrize("wide", [True, False])
+@pytest.mark.parametrize("pattern", ["pairs", "mixed", "hot", "overflow"])
+def test_radix_bucketed_multi_match(hj, oracle, wide, pattern):
+    """k_join_b's repeated build keys: every copy of a repeated key is marked
+    by the suspects' chain checks, and probe rows whose first match is marked
+    write all their pairs by a chain walk -- pairs (2 copies), a mix of 2..6
+    copies (C1-ref-like), one key 40x, and copies crowding home buckets past
+    their 4 slots (chains over several buckets).  int64 rows; the same
+    shapes with i32 rows run k_join_u's per-row walks."""
+    n = 60000
+    rng = np.random.default_rng(1234 + len(pattern) + (7 if wide else 0))
+    base = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
+    rk = base.copy()
+    # (repeats stay under a quarter of the build rows: the sample then keeps
+    # k_join_b, asserted below)
+    if pattern == "pairs":
+        rk[1:n // 4:2] = rk[0:n // 4:2][: len(rk[1:n // 4:2])]
+    elif pattern == "mixed":
+        reps = rng.integers(1, 7, size=n // 8)
+        rk[: n // 8] = np.repeat(base[n // 8: n // 4], reps)[: n // 8]
+    elif pattern == "hot":
+        rk[500:540] = rk[499]
+    else:   # keys crowding one home bucket region: many copies of few keys
+        rk[:4000] = np.repeat(base[:400], 10)
+    rng.shuffle(rk)
+    sk = np.concatenate([rng.choice(rk, size=n // 2), rng.integers(1, 1 << 30, size=n // 2)])
+    rp = np.arange(n, dtype=np.int64) * 3 + 1
+    sp = np.arange(len(sk), dtype=np.int64) * 5 + 2
+    if wide:
+        o = run(hj, rk, rp, sk, sp, 6)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
+    else:
+        o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 6)
+        ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
+        assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
+    assert hj.has_duplicates()
+    assert hj.join_kernel == ("k_join_b" if wide else "k_join_u")
