@@ -135,7 +135,9 @@ int hj_ctx_join_kernel(hj_ctx *ctx);
  * probe:  @probeRelation                       (join_v2.mlir:149-199)
  * d_count (device uint64): set to M, the exact number of result rows, even
  * when M > out_cap (rows past out_cap are dropped; re-run with a larger
- * output).  The counter is zeroed by the call. */
+ * output).  The counter is zeroed by the call.  Bit 63 set means an internal
+ * work list overflowed (a sizing bug, never expected): the result is invalid
+ * and the host entry points return HJ_ERR_CAPACITY for it. */
 
 /* 64-bit key / 64-bit payload column pairs (north_star types). */
 int hj_dev_build_i64(hj_ctx *ctx, const int64_t *rkey, const int64_t *rpay, int64_t n, void *stream);

@@ -755,6 +755,7 @@ int host_probe_all(hj_ctx *c, int layout, const hj::SrcDev &probe, size_t esz, i
         HJ_TRY(do_probe(c, layout, probe, o_r, o_s, cap, (uint64_t *)c->dcount, false, st));
         HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
         HJ_HIP(hipStreamSynchronize(st));
+        if (cnt >> 63) HJ_FAIL(HJ_ERR_CAPACITY, "probe: internal work list overflow (count flagged)");
         if ((int64_t)cnt <= cap) break;
         cap = (int64_t)cnt;   // exact M known: second pass fits
     }

@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
             // general path: k_probe_slow takes this tile
             if (threadIdx.x == 0) {
                 const unsigned long long j = atomicAdd(&t.meta[3], 1ull);
-                if (j < slow_cap) slow[j] = (unsigned)(q * kXcdGroups + g);   // (sized so it always is)
+                if (j < slow_cap) slow[j] = (unsigned)(q * kXcdGroups + g);   // (sized so it always is; else k_probe_slow flags the count)
             }
             continue;
         }
@@ -372,6 +372,9 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
     const slot_t *sl = (const slot_t *)t.slots;
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
     const unsigned long long ntiles = t.meta[3] < slow_cap ? t.meta[3] : slow_cap;
+    // an undersized slow list would drop tiles: report it through the count
+    // (bit 63, never a real M) rather than return a short result
+    if (blockIdx.x == 0 && threadIdx.x == 0 && t.meta[3] > slow_cap) atomicOr(out.counter, 1ull << 63);
     for (unsigned long long j = blockIdx.x; j < ntiles; j += gridDim.x) {
         if (threadIdx.x == 0) st_n = 0u;
         const unsigned id = slow[j];

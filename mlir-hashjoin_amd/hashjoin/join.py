@@ -288,6 +288,8 @@ class HashJoin:
             out_s = torch.empty(cap, dtype=dt, device=self.device)
             cnt = self.probe_relation(skey, spay, out_r, out_s, stream=stream)
             m = int(cnt.item())
+            if m < 0:   # bit 63: an internal work list overflowed (hj.h)
+                raise RuntimeError("hash join: internal work list overflow (count flagged)")
             if m <= cap:
                 return out_r[:m], out_s[:m]
             cap = m
