@@ -188,9 +188,11 @@ def _dj_worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=3000, NS=5001, frac=0.9, seed=31, s_parts=3, world=3, max_rows=113),  # S in 3 batches
     dict(dist="uniform", NR=2000, NS=2500, hi=200, seed=32, s_parts=4, capacity=1000),  # parts overflow the output
     dict(dist="pkfk", NR=7, NS=2, frac=1.0, seed=33, s_parts=5, world=2),               # empty parts
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=34, world=1),                    # identity exchange
+    dict(dist="uniform", NR=2000, NS=2500, hi=300, seed=35, world=1, s_parts=2, capacity=700),
 ], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
         "tiny_4ranks", "known_build_size", "known_build_size_replicate", "s_parts3", "s_parts_overflow",
-        "s_parts_empty"])
+        "s_parts_empty", "one_rank", "one_rank_s_parts2"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
