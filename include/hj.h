@@ -169,6 +169,35 @@ int hj_dev_partition_tuples_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n, i
 /* Owning partition of one key (host-side, same function as the kernels). */
 int hj_partition_of(int64_t key, int nparts);
 
+/* Folded routing (north_star: "probe tuples routed by the same radix"): a
+ * row's owner AND its receiver's first radix-pass bin are the top
+ * log2(nranks) + sub_bits bits of the radix join's own key hash, so the
+ * received tuples are already first-pass partitioned and the receiver runs
+ * one local pass fewer per relation (R and S).
+ * hj_route_plan: sub_bits for a join of n_build_global build rows over nranks
+ * ranks (a power of two, <= 64); *sub_bits = 0 when the fold does not apply
+ * (small or non-radix local build sides, other rank counts): route with
+ * hj_dev_partition_* then.  The same value on every rank. */
+int hj_route_plan(int64_t n_build_global, int nranks, int *sub_bits);
+/* out_tuples (2n int64): packed {key, pay} grouped by part = owner << sub_bits
+ * | bin (<= 512 parts), parts in order; d_counts (nranks << sub_bits uint64):
+ * part sizes.  One exact partition pass (line-tailed, like a radix pass) after
+ * a key histogram. */
+int hj_dev_route_i64(hj_ctx *ctx, const int64_t *key, const int64_t *pay, int64_t n, int nranks, int sub_bits,
+                     int64_t *out_tuples, uint64_t *d_counts, void *stream);
+/* Build from routed tuples: nsrc sources' rows one after another, each
+ * source's grouped by bin 0 .. 2^sub_bits - 1; d_counts (device, nsrc x
+ * 2^sub_bits uint64, row s = source s's bin sizes).  nranks, sub_bits as
+ * routed. */
+int hj_dev_build_routed_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n, const uint64_t *d_counts, int nsrc,
+                            int nranks, int sub_bits, void *stream);
+/* Probe routed tuples of bins [bin0, bin0 + nbins) only (the part of the probe
+ * side that has arrived), laid out as for the build; d_counts nsrc x nbins.
+ * Output as hj_dev_probe_i64. */
+int hj_dev_probe_routed_i64(hj_ctx *ctx, const int64_t *tuples, int64_t n, const uint64_t *d_counts, int nsrc,
+                            int bin0, int nbins, int64_t *out_r, int64_t *out_s, int64_t out_cap, uint64_t *d_count,
+                            void *stream);
+
 /* Deterministic synthetic relations (counter-based, so any slice of a
  * global relation can be generated independently on any GPU). */
 int hj_dev_gen_pkfk_i64(uint64_t seed, int64_t NR, uint64_t hit_threshold,

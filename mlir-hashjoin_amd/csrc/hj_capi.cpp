@@ -128,6 +128,7 @@ struct hj_ctx {
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
+    Buf route_hist, route_sums;               // folded routing: (bin, workgroup) slot bases, scan sums
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -165,6 +166,7 @@ struct hj_ctx {
     // the last radix probe's shape, for hj_ctx_join_kernel (the kernel itself
     // follows from these and the build-time sample in meta[2..3])
     bool join_ran = false, join_wide = false, join_stream = false;
+    bool routed = false;   // the current build came from hj_dev_build_routed_i64 (plan.skip owner bits)
     hipStream_t join_st = nullptr;
 };
 
@@ -320,6 +322,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->used = choose_strategy(c, src.n);
     c->probe_used = -1;
     c->join_ran = false;
+    c->routed = false;
     c->memo.valid = false;   // (hj_count_*'s kept table is gone)
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
@@ -1009,7 +1012,8 @@ void hj_ctx_destroy(hj_ctx *c) {
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->runs, &sb->rstart}) free_buf(*b);
     for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums,
-                   &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums})
+                   &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
+                   &c->route_hist, &c->route_sums})
         free_buf(*b);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
@@ -1194,6 +1198,126 @@ int hj_dev_partition_i64(hj_ctx *c, const int64_t *key, const int64_t *pay, int6
 int hj_dev_partition_tuples_i64(hj_ctx *c, const int64_t *tuples, int64_t n, int nparts, int64_t *out_tuples,
                                 uint64_t *d_counts, void *stream) {
     return do_partition(c, src_packed(tuples, n), nparts, out_tuples, d_counts, (hipStream_t)stream);
+}
+
+int hj_route_plan(int64_t n_build_global, int nranks, int *sub_bits) {
+    if (!sub_bits) HJ_FAIL(HJ_ERR_ARG, "null argument");
+    *sub_bits = 0;
+    if (nranks < 1 || nranks > hj::kMaxRouteSources || (nranks & (nranks - 1)) || n_build_global < 0)
+        return HJ_OK;
+    const int g = ceil_log2((unsigned long long)nranks);
+    const int64_t local = (n_build_global + nranks - 1) / nranks;
+    if (local < kRadixMinRows || g >= 9) return HJ_OK;
+    const int t = hj::radix_plan(local, 0, true).total_bits;
+    const int b1 = 9 - g < t - 1 ? 9 - g : t - 1;
+    if (b1 >= 1 && t - b1 <= 9) *sub_bits = b1;
+    return HJ_OK;
+}
+
+int hj_dev_route_i64(hj_ctx *c, const int64_t *key, const int64_t *pay, int64_t n, int nranks, int sub_bits,
+                     int64_t *out_tuples, uint64_t *d_counts, void *stream) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (n > 0 && (!key || !pay || !out_tuples)) HJ_FAIL(HJ_ERR_ARG, "bad route input");
+    if (!d_counts) HJ_FAIL(HJ_ERR_ARG, "null counts");
+    if (nranks < 1 || (nranks & (nranks - 1)) || sub_bits < 1) HJ_FAIL(HJ_ERR_ARG, "nranks: a power of two; sub_bits >= 1");
+    const int rbits = ceil_log2((unsigned long long)nranks) + sub_bits;
+    if (rbits > 9) HJ_FAIL(HJ_ERR_ARG, "nranks << sub_bits must be <= 512");
+    hipStream_t st = (hipStream_t)stream;
+    HJ_TRY(set_device(c));
+    const size_t hw = hj::radix_route_scratch(n, rbits);
+    HJ_TRY(ensure_buf(c->route_hist, hw * 8));
+    HJ_TRY(ensure_buf(c->route_sums, hj::exclusive_scan_sums(hw) * 8));
+    record(c, kEvPart0, st);
+    HJ_HIP(hj::radix_route(src_cols64(key, pay, n), rbits, out_tuples, (unsigned long long *)d_counts,
+                           (unsigned long long *)c->route_hist.p, (unsigned long long *)c->route_sums.p, st));
+    record(c, kEvPart1, st);
+    c->rec[3] = c->timing;
+    return HJ_OK;
+}
+
+int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const uint64_t *d_counts, int nsrc,
+                            int nranks, int sub_bits, void *stream) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (n < 0 || (n > 0 && !tuples) || !d_counts) HJ_FAIL(HJ_ERR_ARG, "bad routed build relation");
+    if (nsrc < 1 || nsrc > hj::kMaxRouteSources || nranks < 1 || (nranks & (nranks - 1)) || sub_bits < 1 ||
+        sub_bits > 9)
+        HJ_FAIL(HJ_ERR_ARG, "bad routed layout");
+    hipStream_t st = (hipStream_t)stream;
+    HJ_TRY(set_device(c));
+    HJ_TRY(ensure_meta(c, 64));
+    // this rank's plan: the routing's bins are its first pass (skip = the
+    // owner bits above them), one local pass of <= 9 bits below them
+    hj::RadixPlan pl = hj::radix_plan(n, 0, true);
+    int t = pl.total_bits;
+    if (t < sub_bits + 1) t = sub_bits + 1;
+    if (t > sub_bits + 9) t = sub_bits + 9;
+    pl.passes = 2;
+    pl.bits[0] = sub_bits;
+    pl.bits[1] = t - sub_bits;
+    pl.bits[2] = 0;
+    pl.pbl[0] = 10;   // (sizes the ping set, whose run arrays list the routed rows)
+    pl.pbl[1] = hj::kFinalPbl;
+    pl.pbl[2] = 0;
+    pl.total_bits = t;
+    pl.skip = ceil_log2((unsigned long long)nranks);
+    c->layout = kWide;
+    c->n_build = n;
+    c->used = HJ_STRATEGY_RADIX;
+    c->dual = false;
+    c->probe_used = -1;
+    c->join_ran = false;
+    c->memo.valid = false;
+    c->plan = pl;
+    c->routed = true;
+    HJ_TRY(ensure_radix_scratch(c, c->rset, n, 16, pl));
+    record(c, kEvInit0, st);
+    HJ_HIP(hipMemsetAsync(c->meta, 0, 4 * sizeof(unsigned long long), st));
+    record(c, kEvInit1, st);
+    HJ_HIP(hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, 1 << sub_bits, pl,
+                                      radix_work(c), bucket_set(c->rset), st));
+    HJ_HIP(hj::radix_sample(true, pl, bucket_set(c->rset), c->meta + 2, st));
+    record(c, kEvBuild1, st);
+    c->rec[0] = c->rec[1] = c->timing;
+    return HJ_OK;
+}
+
+int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const uint64_t *d_counts, int nsrc,
+                            int bin0, int nbins, int64_t *out_r, int64_t *out_s, int64_t out_cap, uint64_t *d_count,
+                            void *stream) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (!d_count) HJ_FAIL(HJ_ERR_ARG, "null count pointer");
+    if (c->layout != kWide || c->used != HJ_STRATEGY_RADIX || !c->routed)
+        HJ_FAIL(HJ_ERR_STATE, "probe_routed needs a routed build");
+    if (n < 0 || (n > 0 && !tuples) || !d_counts) HJ_FAIL(HJ_ERR_ARG, "bad routed probe relation");
+    if (out_cap < 0 || (out_cap > 0 && (!out_r || !out_s))) HJ_FAIL(HJ_ERR_ARG, "bad output");
+    const int F = 1 << c->plan.bits[0];
+    if (nsrc < 1 || nsrc > hj::kMaxRouteSources || bin0 < 0 || nbins < 1 || bin0 + nbins > F)
+        HJ_FAIL(HJ_ERR_ARG, "bad routed layout");
+    hipStream_t st = (hipStream_t)stream;
+    HJ_TRY(set_device(c));
+    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+    c->probe_used = HJ_STRATEGY_RADIX;
+    HJ_TRY(ensure_radix_scratch(c, c->sset, n, 16, c->plan));
+    record(c, kEvProbe0, st);
+    HJ_HIP(hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, nbins, c->plan,
+                                      radix_work(c), bucket_set(c->sset), st));
+    record(c, kEvProbeMid, st);
+    // bins [bin0, bin0 + nbins): partitions [bin0, bin0 + nbins) << bits[1] of R
+    hj::BucketSet r = bucket_set(c->rset);
+    r.rstart += (size_t)bin0 << c->plan.bits[1];
+    const bool stream_shape = n >= 8 * c->n_build;
+    HJ_HIP(hj::radix_join(true, c->plan, radix_work(c), r, bucket_set(c->sset), c->sset.max_runs,
+                          (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, out_cap,
+                          (unsigned long long *)d_count, c->meta + 1, false, st, c->meta + 2, stream_shape,
+                          nbins << c->plan.bits[1]));
+    c->join_ran = true;
+    c->join_wide = true;
+    c->join_stream = stream_shape;
+    c->join_st = st;
+    record(c, kEvProbe1, st);
+    c->rec[2] = c->timing;
+    c->rec_mid = c->timing;
+    return HJ_OK;
 }
 
 int hj_partition_of(int64_t key, int nparts) {

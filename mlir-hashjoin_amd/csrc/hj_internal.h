@@ -128,11 +128,18 @@ size_t probe_tiles_xcd(unsigned long long max_runs);
 // until a partition's build rows fit one workgroup's LDS table, then joins
 // partition pairs in LDS.  A pass writes rows into fixed-size buckets (one
 // partition per bucket, bucket chaining): no histogram pass, no global scan.
+// The radix join's key hash: partitions, passes' bins and LDS slots are its
+// bit fields from the top down (odd multiplier: a bijection of the key).
+__host__ __device__ __forceinline__ unsigned long long radix_hash(unsigned long long k) {
+    return k * 0x9E3779B97F4A7C15ull;
+}
+
 struct RadixPlan {
     int passes;       // 1..3 partition passes
     int bits[3];      // fan-out bits per pass (<= 9 each)
     int pbl[3];       // log2 rows per bucket written by each pass
     int total_bits;   // P = 2^total_bits partitions
+    int skip = 0;     // top hash bits above the partition bits (the owning GPU of a folded routing)
 };
 
 // One pass's output: packed rows in buckets of 2^pbl rows; bucket j holds
@@ -142,6 +149,7 @@ struct RadixPlan {
 // runs[rstart[p] .. rstart[p+1]).  Consumers map one wave to one run, so a
 // partly filled bucket idles at most one wave's tail.
 constexpr int kRunLog = 6;
+constexpr int kFinalPbl = 9;   // 512-row buckets for the join's input (8 / 9 / 10+9 measured: profiles/r01_bucket_sizes.txt)
 struct BucketSet {
     void *rows;                    // >= max_buckets << pbl rows
     unsigned *bbin, *bfill;        // >= max_buckets
@@ -186,10 +194,28 @@ size_t radix_item_desc_bytes();
 // may be null = "unique"); stream = the probe side is many times the build
 // side (C2): int64 rows take the larger-sub-chunk shape.  The kernel that
 // joins follows from (wide, stream, sample) alone: join_kernel_choice.
+// nparts >= 0: join that many partitions (r.rstart / s.rstart views of a
+// sub-range) instead of the plan's 2^total_bits.
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      const unsigned long long *sample, bool stream);
+                      const unsigned long long *sample, bool stream, int nparts = -1);
+// Folded routing's send side: rows (int64 columns or packed tuples) grouped
+// by the top rbits (<= 9) of radix_hash into out_tuples, exact and contiguous
+// per bin, bins in order; counts[2^rbits] their sizes.  One EXACT partition
+// pass (k_pass's tiles, line tails and loads) behind a key histogram; hist
+// and scan_sums: radix_route_scratch(n, rbits) and exclusive_scan_sums(that)
+// u64 each.
+size_t radix_route_scratch(long long n, int rbits);
+hipError_t radix_route(const SrcDev &src, int rbits, void *out_tuples, unsigned long long *counts,
+                       unsigned long long *hist, unsigned long long *scan_sums, hipStream_t st);
+// Folded multi-GPU routing: `tuples` (packed int64 {key, payload}) were
+// routed by the top pl.skip + pl.bits[0] bits of radix_hash, so they arrive
+// already split into the plan's first-pass segments: for each of nsrc sources
+// in order, that source's rows of segments 0 .. nseg-1 (cnt[s * nseg + b]
+// rows each).  Runs the plan's second pass only (pl.passes == 2) into `out`.
+hipError_t radix_partition_routed(const void *tuples, long long n, const unsigned long long *cnt, int nsrc, int nseg,
+                                  const RadixPlan &pl, const RadixWork &ws, const BucketSet &out, hipStream_t st);
 // After R's partition: sample up to 64 build partitions for repeated keys,
 // adding {rows sampled, rows whose key repeated} into sample[0..1] (zeroed by
 // the caller).  Deterministic for given data.
@@ -202,9 +228,12 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
 // Routing fan-out limit: k_part_scatter (> 512 parts) keeps 12 B of LDS
 // counters per part, k_part_hist 4 B (<= 96 KiB of the 160 KiB).
 constexpr int kMaxRouteParts = 8192;
+constexpr int kMaxRouteSources = 64;   // ranks a folded routing's receiver takes rows from
+// rbits > 0: parts = the top rbits of radix_hash (nparts = 2^rbits), else an
+// fmix64 multiply-shift onto [0, nparts) independent of the radix bits.
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
                             unsigned long long *counts, unsigned long long *cursors,
-                            hipStream_t st);
+                            hipStream_t st, int rbits = 0);
 
 // exclusive scan of a u64 array in place (hj_radix.hip); sums >= exclusive_scan_sums(len)
 hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,

@@ -474,8 +474,11 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
 // ------------------------------------------------------------------ partition
 // Radix partition by a hash independent of the slot hash (fmix64 top word,
 // multiply-shift onto [0, P)), so a partition's keys still spread over its
-// local table.  Used to route R and S rows to their owning GPU.
-__device__ __forceinline__ unsigned part_of(unsigned long long k, unsigned P) {
+// local table.  Used to route R and S rows to their owning GPU.  rbits > 0:
+// the top rbits of the radix join's own key hash instead (P = 2^rbits) --
+// the folded routing, whose parts are (owner, first-pass bin) pairs.
+__device__ __forceinline__ unsigned part_of(unsigned long long k, unsigned P, int rbits) {
+    if (rbits > 0) return (unsigned)(radix_hash(k) >> (64 - rbits));
     return (unsigned)(((fmix64(k) >> 32) * (unsigned long long)P) >> 32);
 }
 
@@ -507,7 +510,7 @@ __device__ __forceinline__ unsigned agg_add(unsigned *cnt, unsigned d, bool vali
 }
 
 template <int FORM>
-__global__ __launch_bounds__(kBlock) void k_part_hist(SrcDev src, unsigned P, unsigned long long *counts) {
+__global__ __launch_bounds__(kBlock) void k_part_hist(SrcDev src, unsigned P, int rbits, unsigned long long *counts) {
     extern __shared__ unsigned lds_hist[];
     for (unsigned i = threadIdx.x; i < P; i += kBlock) lds_hist[i] = 0u;
     __syncthreads();
@@ -519,7 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_part_hist(SrcDev src, unsigned P, un
         for (int i = 0; i < kPartItems; ++i) {
             const long long row = base + (long long)i * kBlock;
             const bool v = row < src.n;
-            const unsigned d = v ? part_of(load_src<FORM>(src, row).k, P) : 0u;
+            const unsigned d = v ? part_of(load_src<FORM>(src, row).k, P, rbits) : 0u;
             if (P <= kAggParts) (void)agg_add(lds_hist, d, v);
             else if (v) atomicAdd(&lds_hist[d], 1u);
         }
@@ -540,7 +543,7 @@ __global__ void k_part_offsets(const unsigned long long *counts, unsigned P, uns
 }
 
 template <int FORM>
-__global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P, ulonglong2 *out,
+__global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P, int rbits, ulonglong2 *out,
                                                          unsigned long long *cursors) {
     extern __shared__ unsigned lds[];   // [0,P) local counts -> ranks, [P,3P) u64 bases
     unsigned *cnt = lds;
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(SrcDev src, unsigned P,
             Tuple tp = load_src<FORM>(src, row);
             k[i] = tp.k;
             p[i] = tp.p;
-            pid[i] = part_of(tp.k, P);
+            pid[i] = part_of(tp.k, P, rbits);
             atomicAdd(&cnt[pid[i]], 1u);
         } else {
             pid[i] = ~0u;
@@ -601,7 +604,7 @@ constexpr int kRouteThreadsS = 256;
 constexpr int kRouteMaxPartsS = 64;
 
 template <int FORM, int TILE, int NT, int MAXP>
-__global__ __launch_bounds__(NT) void k_route_scatter(SrcDev src, unsigned P, ulonglong2 *out,
+__global__ __launch_bounds__(NT) void k_route_scatter(SrcDev src, unsigned P, int rbits, ulonglong2 *out,
                                                       unsigned long long *cursors) {
     constexpr int IT = TILE / NT;
     static_assert(MAXP % 64 == 0 && TILE % NT == 0 && IT % 2 == 0, "route tile shape");
@@ -647,7 +650,7 @@ __global__ __launch_bounds__(NT) void k_route_scatter(SrcDev src, unsigned P, ul
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
         const bool v = pr[i] != ~0u;
-        const unsigned d = v ? part_of(row[i].x, P) : 0u;
+        const unsigned d = v ? part_of(row[i].x, P, rbits) : 0u;
         if (P <= kAggParts) {
             const unsigned r = agg_add(cnt, d, v);
             if (v) pr[i] = (d << 16) | r;
@@ -988,8 +991,9 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
 }
 
 hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
-                            unsigned long long *counts, unsigned long long *cursors, hipStream_t st) {
+                            unsigned long long *counts, unsigned long long *cursors, hipStream_t st, int rbits) {
     const unsigned P = (unsigned)nparts;
+    if (rbits > 0 && (rbits > 13 || P != (1u << rbits))) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * P, st);
     if (e != hipSuccess) return e;
     if (src.n > 0) {
@@ -999,30 +1003,30 @@ hipError_t launch_partition(const SrcDev &src, int nparts, void *out_tuples,
         const unsigned gh = g < (unsigned)cus * 8u ? g : (unsigned)cus * 8u;
         const size_t lds_h = sizeof(unsigned) * P;
         const size_t lds_s = sizeof(unsigned) * ((P + 1) & ~1u) + sizeof(unsigned long long) * P;
-        if (src.form == kCols64) hipLaunchKernelGGL(k_part_hist<kCols64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, counts);
-        else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, counts);
+        if (src.form == kCols64) hipLaunchKernelGGL(k_part_hist<kCols64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, rbits, counts);
+        else if (src.form == kPacked64) hipLaunchKernelGGL(k_part_hist<kPacked64>, dim3(gh), dim3(kBlock), lds_h, st, src, P, rbits, counts);
         else return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_part_offsets, dim3(1), dim3(64), 0, st, counts, P, cursors);
         if (P >= 4u && P <= (unsigned)kRouteMaxPartsS) {
             const unsigned gt = grid_for(src.n, kRouteTileS);
             if (src.form == kCols64)
                 hipLaunchKernelGGL((k_route_scatter<kCols64, kRouteTileS, kRouteThreadsS, kRouteMaxPartsS>), dim3(gt),
-                                   dim3(kRouteThreadsS), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+                                   dim3(kRouteThreadsS), 0, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
             else
                 hipLaunchKernelGGL((k_route_scatter<kPacked64, kRouteTileS, kRouteThreadsS, kRouteMaxPartsS>), dim3(gt),
-                                   dim3(kRouteThreadsS), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+                                   dim3(kRouteThreadsS), 0, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
         } else if (P <= (unsigned)kRouteMaxParts) {
             const unsigned gt = grid_for(src.n, kRouteTile);
             if (src.form == kCols64)
                 hipLaunchKernelGGL((k_route_scatter<kCols64, kRouteTile, kRouteThreads, kRouteMaxParts>), dim3(gt),
-                                   dim3(kRouteThreads), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+                                   dim3(kRouteThreads), 0, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
             else
                 hipLaunchKernelGGL((k_route_scatter<kPacked64, kRouteTile, kRouteThreads, kRouteMaxParts>), dim3(gt),
-                                   dim3(kRouteThreads), 0, st, src, P, (ulonglong2 *)out_tuples, cursors);
+                                   dim3(kRouteThreads), 0, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
         } else if (src.form == kCols64)
-            hipLaunchKernelGGL(k_part_scatter<kCols64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
+            hipLaunchKernelGGL(k_part_scatter<kCols64>, dim3(g), dim3(kBlock), lds_s, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
         else
-            hipLaunchKernelGGL(k_part_scatter<kPacked64>, dim3(g), dim3(kBlock), lds_s, st, src, P, (ulonglong2 *)out_tuples, cursors);
+            hipLaunchKernelGGL(k_part_scatter<kPacked64>, dim3(g), dim3(kBlock), lds_s, st, src, P, rbits, (ulonglong2 *)out_tuples, cursors);
     }
     return hipGetLastError();
 }

@@ -42,7 +42,6 @@ namespace hj {
 namespace {
 
 typedef unsigned long long u64;
-constexpr u64 kGold = 0x9E3779B97F4A7C15ull;
 constexpr int kTile = 4096;        // rows per partition-pass tile (LDS staging: 64 KiB wide)
 constexpr int kPassThreads = 1024; // one workgroup per CU
 constexpr int kPassRows = kTile / kPassThreads;
@@ -53,9 +52,8 @@ constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
 constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
 constexpr int kPassPbl = 10;       // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
-constexpr int kFinalPbl = 9;       // 512-row buckets for the join's input (8 / 9 / 10+9 measured: profiles/r01_bucket_sizes.txt)
 
-__device__ __forceinline__ u64 rhash(u64 k) { return k * kGold; }
+__device__ __forceinline__ u64 rhash(u64 k) { return radix_hash(k); }
 
 // --------------------------------------------------------------- rows
 template <bool WIDE>
@@ -246,6 +244,12 @@ struct PassArgs {
     // run counts and cursors): two memsets and a copy fewer per pass
     u64 *zero_a = nullptr, *zero_b = nullptr;
     u64 zero_n = 0;
+    // EXACT passes (the folded routing): workgroup w writes bin b's rows to
+    // out rows [slot_base[b * G + w], ...) -- exact, contiguous per bin, no
+    // buckets; out_max_rows bounds every write
+    const u64 *slot_base = nullptr;
+    u64 out_max_rows = 0;
+    int hash_top = 0;   // EXACT: bin = the top fbits of the hash (shift = 64 - fbits)
 };
 
 // A bucketed pass's tile: runs [lo, lo + cnt) (cnt <= kTile / 64) of segment seg.
@@ -302,7 +306,12 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, u64 lo, unsigned v, 
 // buckets from a fixed per-tile range instead of the global atomic, 2
 // synthetic rows instead of loads, 4 no row stores (rows and tails), 8 time
 // the phases (s_memtime after each barrier, summed into a.prof).
-template <bool WIDE, int FORM, int ABL = 0>
+// EXACT: the same tiles, counting sort, line tails and pipelined loads, but
+// each (workgroup, bin) writes one exact contiguous slot (k_slot_hist + scan
+// give the bases): rows land grouped by bin with no holes, so a bin's rows
+// can be sent as one message.  A slot's first line is shared with the slot
+// before it (written partly, once); every other line is written whole.
+template <bool WIDE, int FORM, int ABL = 0, bool EXACT = false>
 __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -317,6 +326,9 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ unsigned short sb[kTile];
     __shared__ __attribute__((aligned(16))) unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan],
         nbase[kMaxFan];
+    // EXACT: out row of bin b's position 0 (the slot base rounded down to a
+    // line; positions below cur[b] belong to the slot before)
+    __shared__ u64 cbase[EXACT ? kMaxFan : 1];
     // the tile's fresh buckets: ids s_nb, s_nb + 1, ... (below s_nend)
     __shared__ unsigned s_nb, s_nend;
     // the previous tile's largest bin when it held more than kTile / 8 rows,
@@ -334,8 +346,16 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     T *out = (T *)a.out_rows;
     for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
         cnt[b] = 0u;
-        cur[b] = kNoBucket;
-        fill[b] = PB;   // no open bucket (and no tail: PB is a whole number of lines)
+        if constexpr (EXACT) {
+            const u64 sbase = a.slot_base[(u64)b * gridDim.x + blockIdx.x];
+            const unsigned off0 = (unsigned)(sbase & (L - 1));
+            cbase[b] = sbase - off0;
+            cur[b] = off0;    // the slot's first position
+            fill[b] = off0;   // (no tail rows yet)
+        } else {
+            cur[b] = kNoBucket;
+            fill[b] = PB;   // no open bucket (and no tail: PB is a whole number of lines)
+        }
     }
     // the tile's x-th fresh bucket
     auto fresh = [&](unsigned x) -> unsigned { return s_nb + x < s_nend ? s_nb + x : kNoBucket; };
@@ -344,11 +364,15 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     // shared counter, even one returning atomic per 64 ids, cost 0.25-0.3 ms
     // per 2^28-row pass: waiting for its result also waited for the next
     // tile's loads, profiles/r01_micro_pass2.txt "no bucket atomic".)
-    const unsigned id_end = a.wstart[blockIdx.x + 1];
-    unsigned id_next = a.wstart[blockIdx.x];
+    const unsigned id_end = EXACT ? 0u : a.wstart[blockIdx.x + 1];
+    unsigned id_next = EXACT ? 0u : a.wstart[blockIdx.x];
     // row slot of position p (>= the line start of fill[b]) of bin b's run
     // in the current tile: the open bucket, then the tile's fresh buckets
     auto slot = [&](unsigned b, unsigned p) -> u64 {
+        if constexpr (EXACT) {
+            const u64 o = cbase[b] + p;
+            return o < a.out_max_rows ? o : ~0ull;
+        }
         const unsigned k = p >> a.out_pbl;
         const unsigned bk = k == 0 ? cur[b] : fresh(nbase[b] + k - 1);
         return bk < a.max_buckets ? ((u64)bk << a.out_pbl) + (p & (PB - 1)) : ~0ull;
@@ -357,6 +381,15 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     // close this workgroup's open buckets: write each tail (the bucket's
     // last, partial line); their fill is final
     auto close_all = [&]() {
+        if constexpr (EXACT) {   // the slots' last, partial lines
+            for (unsigned q = threadIdx.x; q < F * (L - 1); q += kPassThreads) {
+                const unsigned b = q / (L - 1), i = q - b * (L - 1);
+                const unsigned f = fill[b], tl = f & (L - 1);
+                const unsigned p = f - tl + i;
+                if (i < tl && p >= cur[b] && cbase[b] + p < a.out_max_rows) out[cbase[b] + p] = tail[q];
+            }
+            return;
+        }
         for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
             const unsigned f = fill[b], tl = f & (L - 1);
             if (cur[b] != kNoBucket && cur[b] < a.max_buckets) {
@@ -552,7 +585,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     c[j] = lane * 8 + j < F ? cv[j] : 0u;
-                    k[j] = c[j] ? (fv[j] + c[j] - 1) >> a.out_pbl : 0u;
+                    k[j] = (!EXACT && c[j]) ? (fv[j] + c[j] - 1) >> a.out_pbl : 0u;
                     s += c[j];
                     sk += k[j];
                 }
@@ -627,6 +660,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             if (i >= tl0) continue;
             const unsigned p = f - tl0 + i;
             if (p >= ((f + cnt[b]) & ~(L - 1))) continue;   // line still incomplete: stays
+            if (EXACT && p < cur[b]) continue;                 // (the slot before's rows)
             const u64 o = slot(b, p);
             if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, tail[q]);
         }
@@ -640,6 +674,10 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             cnt[b] = 0u;
             if (!c) continue;
             const unsigned f = fill[b];
+            if constexpr (EXACT) {
+                fill[b] = f + c;
+                continue;
+            }
             const unsigned k = (f + c - 1) >> a.out_pbl;
             if (k) {
                 // the replaced open bucket is full (all its lines stored);
@@ -669,10 +707,12 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
     }
     close_all();
-    // ids of the range left unused are holes for the bucket listing
-    if (threadIdx.x == 63) s_hole = id_next;
-    __syncthreads();
-    for (unsigned i = s_hole + threadIdx.x; i < id_end; i += kPassThreads) a.bbin[i] = kNoBucket;
+    if constexpr (!EXACT) {
+        // ids of the range left unused are holes for the bucket listing
+        if (threadIdx.x == 63) s_hole = id_next;
+        __syncthreads();
+        for (unsigned i = s_hole + threadIdx.x; i < id_end; i += kPassThreads) a.bbin[i] = kNoBucket;
+    }
     if constexpr ((ABL & 8) != 0) {
         if (threadIdx.x == 0 && a.prof)
             for (int k = 0; k < 6; ++k) a.prof[blockIdx.x * 8 + k] = ph[k];
@@ -2559,17 +2599,90 @@ unsigned long long radix_join_items(const RadixPlan &pl, unsigned long long s_ru
     return s_runs / chr + (1ull << pl.total_bits) + 2;
 }
 
-// Partition one relation into the plan's 2^total_bits partitions: bucket
-// rows in `out` (with runs / rstart by partition).  ws.tmp is the ping set
-// of multi-pass plans.  Asynchronous; no allocation.
-hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
-                           const BucketSet &out, hipStream_t st) {
+namespace {
+// Bin sizes of every (bin, workgroup) pair of an EXACT pass over the same
+// tiles: hist[b * G + w] (k_pass's tile ranges, bin = the top fbits of the
+// hash), zeroed by the kernel itself.
+template <bool WIDE, int FORM>
+__global__ __launch_bounds__(1024) void k_slot_hist(PassArgs a, u64 *hist) {
+    typedef Row<WIDE> R;
+    __shared__ unsigned c[kMaxFan];
+    const unsigned F = 1u << a.fbits;
+    for (unsigned b = threadIdx.x; b < F; b += 1024) c[b] = 0u;
+    __syncthreads();
+    const unsigned T_ = (unsigned)((a.n + kTile - 1) / kTile);
+    const unsigned t0 = (unsigned)((u64)blockIdx.x * T_ / gridDim.x);
+    const unsigned t1 = (unsigned)((u64)(blockIdx.x + 1) * T_ / gridDim.x);
+    const u64 r0 = (u64)t0 * kTile, r1 = (u64)t1 * kTile < a.n ? (u64)t1 * kTile : a.n;
+    for (u64 r = r0 + threadIdx.x; r < r1; r += 1024) {
+        u64 key;
+        if constexpr (FORM == kCols64) key = ((const u64 *)a.in.key)[r];
+        else key = R::key(((const typename R::T *)a.in.key)[r]);
+        atomicAdd(&c[(unsigned)(rhash(key) >> a.shift) & (F - 1)], 1u);
+    }
+    __syncthreads();
+    for (unsigned b = threadIdx.x; b < F; b += 1024) hist[(u64)b * gridDim.x + blockIdx.x] = c[b];
+}
+
+// Bin sizes from the scanned slot bases.
+__global__ __launch_bounds__(256) void k_slot_counts(const u64 *base, unsigned F, unsigned G, u64 n, u64 *counts) {
+    const unsigned b = blockIdx.x * 256 + threadIdx.x;
+    if (b < F) counts[b] = (b + 1 < F ? base[(u64)(b + 1) * G] : n) - base[(u64)b * G];
+}
+}  // namespace
+
+size_t radix_route_scratch(long long n, int rbits) {
+    const u64 G = pass_grid((u64)(n > 0 ? n : 1));
+    return (size_t)(((u64)1 << rbits) * G + 1);
+}
+
+hipError_t radix_route(const SrcDev &src, int rbits, void *out_tuples, unsigned long long *counts,
+                       unsigned long long *hist, unsigned long long *scan_sums, hipStream_t st) {
+    if (rbits < 1 || rbits > 9 || (src.form != kCols64 && src.form != kPacked64)) return hipErrorInvalidValue;
     const u64 n = (u64)(src.n > 0 ? src.n : 0);
-    int nseg = 1;
-    int shift = 64;
-    const BucketSet *prev = nullptr;
+    const unsigned F = 1u << rbits;
+    if (n == 0) return hipMemsetAsync(counts, 0, F * sizeof(u64), st);
+    const unsigned G = pass_grid(n);
+    PassArgs a;
+    a.in = src;
+    a.n = n;
+    a.cols_aligned = ((((uintptr_t)src.key) | ((uintptr_t)src.pay)) & 15) == 0;
+    a.in_rows = nullptr;
+    a.in_runs = nullptr;
+    a.in_rstart = nullptr;
+    a.in_max_rows = a.in_max_runs = 0;
+    a.tile_start = nullptr;
+    a.tdesc = nullptr;
+    a.nseg = 1;
+    a.out_rows = out_tuples;
+    a.bbin = a.bfill = a.nb = nullptr;
+    a.wstart = nullptr;
+    a.max_buckets = 0;
+    a.out_pbl = 0;
+    a.shift = 64 - rbits;
+    a.fbits = rbits;
+    a.zero_n = 0;
+    a.slot_base = (const u64 *)hist;
+    a.out_max_rows = n;
+    if (src.form == kCols64) hipLaunchKernelGGL((k_slot_hist<true, kCols64>), dim3(G), dim3(1024), 0, st, a, (u64 *)hist);
+    else hipLaunchKernelGGL((k_slot_hist<true, kPackedRow>), dim3(G), dim3(1024), 0, st, a, (u64 *)hist);
+    scan_u64((u64 *)hist, (u64)F * G, (u64 *)scan_sums, st);
+    hipLaunchKernelGGL(k_slot_counts, dim3(blocks_for(F, 256)), dim3(256), 0, st, (const u64 *)hist, F, G, n,
+                       (u64 *)counts);
+    if (src.form == kCols64) hipLaunchKernelGGL((k_pass<true, kCols64, 0, true>), dim3(G), dim3(kPassThreads), 0, st, a);
+    else hipLaunchKernelGGL((k_pass<true, kPackedRow, 0, true>), dim3(G), dim3(kPassThreads), 0, st, a);
+    return hipGetLastError();
+}
+
+namespace {
+// Passes first .. pl.passes - 1 of plan pl; the first of them reads `prev`
+// (a bucket set over nseg segments) or, when prev is null, the source rows.
+hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl, int first, const BucketSet *prev,
+                        int nseg, const RadixWork &ws, const BucketSet &out, hipStream_t st) {
+    int shift = 64 - pl.skip;
+    for (int pass = 0; pass < first; ++pass) shift -= pl.bits[pass];
     const unsigned grid = pass_grid(n > 0 ? n : 1);
-    for (int pass = 0; pass < pl.passes; ++pass) {
+    for (int pass = first; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
         shift -= fb;
         const BucketSet &dst = ((pl.passes - 1 - pass) % 2) == 0 ? out : ws.tmp;
@@ -2655,11 +2768,84 @@ hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, co
     return hipSuccess;
 }
 
+// Routed rows as a first-pass bucket set: tuples hold, for each source in
+// order, that source's rows of segments 0 .. nseg-1 in segment order,
+// cnt[s * nseg + b] of them; segment b lists its rows as runs (<= 64 rows,
+// row << 7 | count), source by source.  One block per segment.
+__global__ __launch_bounds__(256) void k_routed_list(const u64 *cnt, int nsrc, int nseg, u64 *runs, u64 *rstart,
+                                                     u64 max_runs) {
+    __shared__ u64 tot[kMaxRouteSources], before[kMaxRouteSources];
+    __shared__ u64 runs_before, runs_all;
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < nsrc; i += 256) tot[i] = before[i] = 0ull;
+    if (threadIdx.x == 0) runs_before = runs_all = 0ull;
+    __syncthreads();
+    u64 rb = 0, ra = 0;
+    for (int i = threadIdx.x; i < nsrc * nseg; i += 256) {
+        const int s = i / nseg, bb = i - s * nseg;
+        const u64 c = cnt[i], r = (c + 63) >> kRunLog;
+        atomicAdd(&tot[s], c);
+        ra += r;
+        if (bb < b) {
+            atomicAdd(&before[s], c);
+            rb += r;
+        }
+    }
+    if (rb) atomicAdd(&runs_before, rb);
+    if (b == 0 && ra) atomicAdd(&runs_all, ra);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        rstart[b] = runs_before;
+        if (b == 0) rstart[nseg] = runs_all;
+    }
+    // source s's rows of segment b: row base = the rows of sources < s, then
+    // s's rows of segments < b; its runs follow those of sources < s
+    u64 row0 = 0, run0 = runs_before;
+    for (int s = 0; s < nsrc; ++s) {
+        const u64 c = cnt[(u64)s * nseg + b], base = row0 + before[s];
+        const u64 r = (c + 63) >> kRunLog;
+        for (u64 j = threadIdx.x; j < r; j += 256) {
+            const u64 len = c - (j << kRunLog) < 64 ? c - (j << kRunLog) : 64;
+            if (run0 + j < max_runs) runs[run0 + j] = ((base + (j << kRunLog)) << 7) | len;
+        }
+        row0 += tot[s];
+        run0 += r;
+    }
+}
+}  // namespace
+
+// Partition one relation into the plan's 2^total_bits partitions: bucket
+// rows in `out` (with runs / rstart by partition).  ws.tmp is the ping set
+// of multi-pass plans.  Asynchronous; no allocation.
+hipError_t radix_partition(const SrcDev &src, bool wide, const RadixPlan &pl, const RadixWork &ws,
+                           const BucketSet &out, hipStream_t st) {
+    const u64 n = (u64)(src.n > 0 ? src.n : 0);
+    return radix_passes(src, n, wide, pl, 0, nullptr, 1, ws, out, st);
+}
+
+hipError_t radix_partition_routed(const void *tuples, long long n, const unsigned long long *cnt, int nsrc, int nseg,
+                                  const RadixPlan &pl, const RadixWork &ws, const BucketSet &out, hipStream_t st) {
+    if (pl.passes != 2 || nsrc < 1 || nsrc > kMaxRouteSources || nseg < 1) return hipErrorInvalidValue;
+    // the routed listing borrows the ping set's run arrays (a 2-pass plan's
+    // second pass writes `out`, not ws.tmp)
+    hipLaunchKernelGGL(k_routed_list, dim3(nseg), dim3(256), 0, st, (const u64 *)cnt, nsrc, nseg, ws.tmp.runs,
+                       ws.tmp.rstart, (u64)ws.tmp.max_runs);
+    BucketSet in = ws.tmp;
+    in.rows = const_cast<void *>(tuples);
+    in.max_rows = (u64)(n > 0 ? n : 0);
+    SrcDev src{};
+    src.key = tuples;
+    src.pay = nullptr;
+    src.n = n;
+    src.form = kPacked64;
+    return radix_passes(src, (u64)(n > 0 ? n : 0), true, pl, 1, &in, nseg, ws, out, st);
+}
+
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
-                      const unsigned long long *sample, bool stream) {
-    const int P = 1 << pl.total_bits;
+                      const unsigned long long *sample, bool stream, int nparts) {
+    const int P = nparts >= 0 ? nparts : 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     if (pl.pbl[pl.passes - 1] != kFinalPbl) return hipErrorInvalidValue;
     // persistent grids: two workgroups per CU (LDS-limited); i32 rows' fast
@@ -2697,7 +2883,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
     // the hash bits right below the partition bits: LDS slot / bucket
-    a.tshift = 64 - pl.total_bits - (wide ? kTableLog : kTableLogNarrow);
+    a.tshift = 64 - pl.skip - pl.total_bits - (wide ? kTableLog : kTableLogNarrow);
     a.out_r = out_r;
     a.out_s = out_s;
     a.cap = cap;

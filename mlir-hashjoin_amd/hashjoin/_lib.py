@@ -76,6 +76,10 @@ def _load():
         "hj_dev_partition_i64": (_int, [_vp, _vp, _vp, _i64, _int, _vp, _vp, _vp]),
         "hj_dev_partition_tuples_i64": (_int, [_vp, _vp, _i64, _int, _vp, _vp, _vp]),
         "hj_partition_of": (_int, [_i64, _int]),
+        "hj_route_plan": (_int, [_i64, _int, C.POINTER(C.c_int)]),
+        "hj_dev_route_i64": (_int, [_vp, _vp, _vp, _i64, _int, _int, _vp, _vp, _vp]),
+        "hj_dev_build_routed_i64": (_int, [_vp, _vp, _i64, _vp, _int, _int, _int, _vp]),
+        "hj_dev_probe_routed_i64": (_int, [_vp, _vp, _i64, _vp, _int, _int, _int, _vp, _vp, _i64, _vp, _vp]),
         "hj_dev_gen_pkfk_i64": (_int, [_u64, _i64, _u64, _i64, _i64, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
         "hj_zipf_params": (_int, [_i64, C.c_double, C.POINTER(C.c_double)]),
         "hj_dev_gen_zipf_i64": (_int, [_u64, _i64, C.c_double, _i64, _i64, _vp, _vp, _vp]),

@@ -7,7 +7,12 @@ Hash-Join" and "Joining skewed data" as left out); north_star adds this path
 
   SHUFFLE (large build sides)
   1. every rank radix-partitions its slice of R and of S by the owner hash
-     (hj_dev_partition_*: one HIP histogram + scatter pass each),
+     (hj_dev_partition_*: one HIP histogram + scatter pass each).  FOLDED
+     (hj_route_plan > 0: a power-of-two world and a radix-sized local build):
+     the owner and the receiver's first radix-pass bin are the top bits of
+     the join's own key hash (hj_dev_route_i64), so every rank receives its
+     rows already first-pass partitioned and builds / probes with one local
+     pass (hj_dev_build_routed_i64 / hj_dev_probe_routed_i64) instead of two,
   2. per relation, one all-to-all of the per-owner counts (world int64),
   3. per relation, one batched group of point-to-point messages (RCCL
      grouped send/recv) of packed 16-B {key, payload} tuples, started
@@ -159,6 +164,66 @@ class Exchange:
         return self.recv
 
 
+class RoutedExchange:
+    """The folded routing's transfer.  send holds, destination by destination,
+    that destination's bins 0 .. F-1 in order; counts (world * F) their sizes.
+    The bin counts are exchanged (one all-to-all of world * F int64), then the
+    rows move in `parts` batches: part k = bins [bounds[k], bounds[k + 1]) of
+    every source, source by source -- whole first-pass segments, so part k can
+    be partitioned and joined as soon as it has arrived.  part_counts[k]
+    (device, nsrc x bins) describes part k's layout for the routed build /
+    probe."""
+
+    def __init__(self, send, counts, nbins, group=None, max_rows=None, self_p2p=False, parts=1):
+        world = dist.get_world_size(group)
+        if counts.numel() != world * nbins:
+            raise ValueError("one count per (rank, bin) required")
+        max_rows = MAX_ROWS_PER_ROUND if max_rows is None else int(max_rows)
+        parts = max(1, min(int(parts), nbins))
+        counts = counts.contiguous().view(world, nbins)
+        recv_counts = torch.empty_like(counts)
+        dist.all_to_all_single(recv_counts, counts, group=group)
+        host = torch.stack([counts, recv_counts]).cpu()
+        send_c, recv_c = host[0], host[1]
+        self.send = send
+        self.bounds = [nbins * k // parts for k in range(parts + 1)]
+        self.in_rows = send_c.sum(1).tolist()
+        self.out_rows = recv_c.sum(1).tolist()
+        dest_off = [int(send_c[:d].sum()) for d in range(world)]
+        self.part_counts = []
+        self._parts = []
+        alias = world == 1 and not self_p2p
+        self.recv = send[:self.out_rows[0]] if alias else torch.empty((sum(self.out_rows), 2), dtype=torch.int64,
+                                                                         device=send.device)
+        base = 0
+        for k in range(parts):
+            b0, b1 = self.bounds[k], self.bounds[k + 1]
+            in_k = send_c[:, b0:b1].sum(1).tolist()
+            out_k = recv_c[:, b0:b1].sum(1).tolist()
+            off_k = [dest_off[d] + int(send_c[d, :b0].sum()) for d in range(world)]
+            recv_k = self.recv[base:base + sum(out_k)]
+            base += sum(out_k)
+            works = [] if alias else _all_to_all_rows(recv_k, send, out_k, in_k, group, max_rows, self_p2p,
+                                                      in_off=off_k)
+            self._parts.append([recv_k, works])
+            self.part_counts.append(recv_counts[:, b0:b1].contiguous())
+
+    @property
+    def parts(self):
+        return len(self._parts)
+
+    def wait_part(self, k):
+        for w in self._parts[k][1]:
+            w.wait()
+        self._parts[k][1] = []
+        return self._parts[k][0]
+
+    def wait(self):
+        for k in range(len(self._parts)):
+            self.wait_part(k)
+        return self.recv
+
+
 def exchange(send_r, counts_r, send_s, counts_s, group=None, max_rows=None):
     """All-to-all-v of two partitioned tuple buffers.
 
@@ -191,13 +256,15 @@ def all_gather_rows(tuples, group=None):
     return torch.cat([full[p * mx:p * mx + counts[p]] for p in range(world)])
 
 
-def _probe_all(hj, tuples, capacity):
-    """Probe into an output sized optimistically, once more at the exact M."""
+def _probe_all(hj, tuples, capacity, probe=None):
+    """Probe into an output sized optimistically, once more at the exact M.
+    probe(tuples, out_r, out_s) -> count tensor (default hj.probe_tuples)."""
+    probe = hj.probe_tuples if probe is None else probe
     cap = max(1, tuples.shape[0] if capacity is None else int(capacity))
     for _ in range(2):
         out_r = torch.empty(cap, dtype=torch.int64, device=tuples.device)
         out_s = torch.empty(cap, dtype=torch.int64, device=tuples.device)
-        cnt = hj.probe_tuples(tuples, out_r, out_s)
+        cnt = probe(tuples, out_r, out_s)
         m = int(cnt.item())
         if m <= cap:
             return out_r[:m], out_s[:m]
@@ -205,26 +272,28 @@ def _probe_all(hj, tuples, capacity):
     raise RuntimeError("distributed join output did not fit after resizing")
 
 
-def _probe_parts(hj, parts, capacity, total, device):
+def _probe_parts(hj, parts, capacity, total, device, probes=None):
     """Probe each received part of S as soon as it is there (callables that
     wait for it), into one output sized `capacity` (default: the S rows
     received); a part whose pairs do not fit what is left is probed again
-    into a buffer of its own at the exact M and the pieces are joined."""
+    into a buffer of its own at the exact M and the pieces are joined.
+    probes[k](tuples, out_r, out_s) probes part k (default hj.probe_tuples)."""
     cap = max(1, total if capacity is None else int(capacity))
     out_r = torch.empty(cap, dtype=torch.int64, device=device)
     out_s = torch.empty(cap, dtype=torch.int64, device=device)
     pos, extra = 0, []
-    for get in parts:
+    for k, get in enumerate(parts):
+        probe = hj.probe_tuples if probes is None else probes[k]
         t = get()
         if t.shape[0] == 0:
             continue
         m = None
         if cap > pos:
-            m = int(hj.probe_tuples(t, out_r[pos:], out_s[pos:]).item())
+            m = int(probe(t, out_r[pos:], out_s[pos:]).item())
             if m <= cap - pos:
                 pos += m
                 continue
-        extra.append(_probe_all(hj, t, m))   # (the rows written past pos are dropped)
+        extra.append(_probe_all(hj, t, m, probe))   # (the rows written past pos are dropped)
     if not extra:
         return out_r[:pos], out_s[:pos]
     return (torch.cat([out_r[:pos]] + [e[0] for e in extra]), torch.cat([out_s[:pos]] + [e[1] for e in extra]))
@@ -239,7 +308,7 @@ S_PARTS = 2
 
 def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phases=None,
                      replicate_max_rows=None, max_rows=None, self_p2p=False, n_build_global=None,
-                     s_parts=None):
+                     s_parts=None, route_bits=None):
     """Join this rank's slices of R and S against every other rank's.
 
     hj: a hashjoin.HashJoin on this rank's GPU (or any object with its
@@ -252,7 +321,9 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     all ranks when the caller knows it (the same value on every rank); it
     saves the all-reduce and host round trip that otherwise decide between
     replicating and shuffling R (~0.15 ms per call).  s_parts: batches the
-    shuffled S moves in (default S_PARTS, 1 at world size 1)."""
+    shuffled S moves in (default S_PARTS, 1 at world size 1).  route_bits: the
+    folded routing's bins per owner (default hj.route_plan's choice; 0 routes
+    by owner only and the receivers run both local passes)."""
     if replicate_max_rows is None:
         replicate_max_rows = REPLICATE_MAX_ROWS
     cuda = rkey.is_cuda
@@ -277,13 +348,40 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
         out = _probe_all(hj, local_s, capacity)
         ev("probed")
         return out
-    _dbg("route", rkey.numel(), skey.numel())
-    send_r, cr = hj.partition(rkey, rpay, dist.get_world_size(group))
-    xr = Exchange(send_r, cr, group, max_rows, self_p2p)
     world = dist.get_world_size(group)
-    send_s, cs = hj.partition(skey, spay, world)
     if s_parts is None:
         s_parts = S_PARTS if world > 1 else 1
+    if route_bits is not None:
+        sub = int(route_bits) if (world & (world - 1)) == 0 else 0
+    else:
+        sub = hj.route_plan(int(n_build_global), world) if hasattr(hj, "route_plan") else 0
+    if sub > 0:
+        # folded: rows arrive first-pass partitioned (one local pass fewer)
+        _dbg("route folded", rkey.numel(), skey.numel(), sub)
+        nb = 1 << sub
+        send_r, cr = hj.route(rkey, rpay, world, sub)
+        xr = RoutedExchange(send_r, cr, nb, group, max_rows, self_p2p)
+        send_s, cs = hj.route(skey, spay, world, sub)
+        xs = RoutedExchange(send_s, cs, nb, group, max_rows, self_p2p, parts=s_parts)
+        ev("routed")
+        recv_r = xr.wait()
+        hj.build_routed(recv_r, xr.part_counts[0], world, sub)
+        ev("built")
+        n_s = sum(xs.out_rows)
+        if phases is not None:
+            phases["rows"] = (recv_r.shape[0], n_s)
+            phases["mode"] = "shuffle"
+            phases["folded"] = True
+        probes = [(lambda t, o_r, o_s, k=k: hj.probe_routed(t, xs.part_counts[k], xs.bounds[k], o_r, o_s))
+                  for k in range(xs.parts)]
+        out = _probe_parts(hj, [lambda k=k: xs.wait_part(k) for k in range(xs.parts)], capacity, n_s, rkey.device,
+                           probes)
+        ev("probed")
+        return out
+    _dbg("route", rkey.numel(), skey.numel())
+    send_r, cr = hj.partition(rkey, rpay, world)
+    xr = Exchange(send_r, cr, group, max_rows, self_p2p)
+    send_s, cs = hj.partition(skey, spay, world)
     xs = Exchange(send_s, cs, group, max_rows, self_p2p, parts=s_parts)
     ev("routed")
     recv_r = xr.wait()

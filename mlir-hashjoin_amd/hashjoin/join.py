@@ -195,6 +195,43 @@ class HashJoin:
               "hj_dev_probe_tuples_i64")
         return count
 
+    # ---- folded routing (hj.h "Folded routing"): the owner and the
+    # receiver's first radix-pass bin from one hash, so receivers skip a pass
+    @staticmethod
+    def route_plan(n_build_global, nranks):
+        """Bin bits per owner for a routed join (0: no fold -- use partition)."""
+        b = C.c_int(0)
+        check(lib.hj_route_plan(int(n_build_global), int(nranks), C.byref(b)), "hj_route_plan")
+        return b.value
+
+    def route(self, key, pay, nranks, sub_bits, stream=None):
+        """(n, 2) tuples grouped by (owner, bin), and the (nranks << sub_bits)
+        part sizes (int64 device tensor)."""
+        _need_cuda(key, pay)
+        n = key.shape[0]
+        out = torch.empty((n, 2), dtype=torch.int64, device=self.device)
+        counts = torch.empty(nranks << sub_bits, dtype=torch.int64, device=self.device)
+        check(lib.hj_dev_route_i64(self._ctx, _ptr(key), _ptr(pay), n, nranks, sub_bits, _ptr(out), _ptr(counts),
+                                   _stream(self.device, stream)), "hj_dev_route_i64")
+        return out, counts
+
+    def build_routed(self, tuples, counts, nranks, sub_bits, stream=None):
+        """Build from routed tuples; counts: (nsrc, 2^sub_bits) int64 device
+        tensor of every source's bin sizes (rows laid out source by source)."""
+        _need_cuda(tuples, counts)
+        check(lib.hj_dev_build_routed_i64(self._ctx, _ptr(tuples), tuples.shape[0], _ptr(counts), counts.shape[0],
+                                          nranks, sub_bits, _stream(self.device, stream)), "hj_dev_build_routed_i64")
+        self.key_bits = 64
+
+    def probe_routed(self, tuples, counts, bin0, out_r, out_s, count=None, stream=None):
+        """Probe routed tuples of bins [bin0, bin0 + counts.shape[1])."""
+        _need_cuda(tuples, counts, out_r, out_s)
+        count = self._count if count is None else count
+        check(lib.hj_dev_probe_routed_i64(self._ctx, _ptr(tuples), tuples.shape[0], _ptr(counts), counts.shape[0],
+                                          bin0, counts.shape[1], _ptr(out_r), _ptr(out_s), out_r.numel(), _ptr(count),
+                                          _stream(self.device, stream)), "hj_dev_probe_routed_i64")
+        return count
+
     def partition(self, key, pay=None, nparts=2, out=None, counts=None, stream=None):
         """Radix-route rows to nparts owners: packed (n, 2) tuples grouped by
         owner + per-owner counts (int64 device tensor)."""

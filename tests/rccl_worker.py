@@ -46,13 +46,18 @@ def main():
                          ("replicate", dict(replicate_max_rows=1 << 21)),
                          ("resize", dict(replicate_max_rows=0, capacity=3, self_p2p=True)),
                          ("s_parts", dict(replicate_max_rows=0, max_rows=2999, self_p2p=True, s_parts=3)),
-                         ("s_parts_overflow", dict(replicate_max_rows=0, self_p2p=True, s_parts=2, capacity=2000))):
+                         ("s_parts_overflow", dict(replicate_max_rows=0, self_p2p=True, s_parts=2, capacity=2000)),
+                         # the folded routing (rows arrive first-pass partitioned)
+                         ("folded", dict(replicate_max_rows=0, route_bits=4, max_rows=3001, self_p2p=True)),
+                         ("folded_parts", dict(replicate_max_rows=0, route_bits=5, self_p2p=True, s_parts=3)),
+                         ("folded_alias", dict(replicate_max_rows=0, route_bits=3, s_parts=2, capacity=1500))):
             ph = {}
             o_r, o_s = distributed_join(hj, d(rk), d(rp), d(sk), d(sp), phases=ph, **kw)
             torch.cuda.synchronize()
             got_r, got_s = o_r.cpu().numpy(), o_s.cpu().numpy()
             assert O.same_multiset(got_r, got_s, er, es), (name, mode, len(got_r), len(er))
             assert ph["mode"] == ("replicate" if mode == "replicate" else "shuffle")
+            assert ph.get("folded", False) == mode.startswith("folded")
             ok += 1
             print(f"ok {name} {mode} M={len(er)}", flush=True)
     # >1 GiB self-exchange at the default piece size: two RCCL messages

@@ -86,3 +86,15 @@ def test_header_compiles_as_c():
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-I", _lib.PKG_ROOT + "/../include",
                         "-x", "c", "-"], input=src, text=True, capture_output=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_route_plan_host():
+    """The folded routing's bin bits (host function, no device needed): 9 -
+    log2(ranks) bits below the owner bits while the local build side is
+    radix-sized, 0 (route by owner only) otherwise."""
+    import hashjoin
+    rp = hashjoin.HashJoin.route_plan
+    assert rp(1 << 28, 1) == 9 and rp(1 << 28, 2) == 8 and rp(1 << 28, 4) == 7 and rp(1 << 28, 8) == 6
+    assert rp(1 << 28, 3) == 0            # not a power of two
+    assert rp(1 << 20, 8) == 0            # 2^17 rows per rank: no radix build there
+    assert rp(1 << 24, 1) == 9            # 2^24: 13 partition bits = 9 + 4

@@ -119,6 +119,48 @@ class _CpuJoin:
         self.calls["build"] += 1
         self.r = t.numpy().copy()
 
+    # the folded routing (hj_dev_route_i64 / _build_routed / _probe_routed):
+    # parts = top log2(nranks) + sub bits of the radix hash key * 0x9E37...15
+    @staticmethod
+    def _rparts(keys, bits):
+        h = keys.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        return (h >> np.uint64(64 - bits)).astype(np.int64)
+
+    def route(self, key, pay, nranks, sub):
+        self.calls["partition"] += 1
+        g = nranks.bit_length() - 1
+        k, p = key.numpy(), pay.numpy()
+        part = self._rparts(k, g + sub)
+        order = np.argsort(part, kind="stable")
+        t = np.stack([k[order], p[order]], axis=1)
+        return torch.from_numpy(np.ascontiguousarray(t)), torch.from_numpy(
+            np.bincount(part, minlength=nranks << sub).astype(np.int64))
+
+    def _check_layout(self, t, counts, bin0, nranks, sub):
+        """Rows of source s, bin bin0 + j sit where counts says, and carry
+        this rank's owner bits and that bin."""
+        g = nranks.bit_length() - 1
+        keys = t.numpy()[:, 0]
+        part = self._rparts(keys, g + sub)
+        c = counts.numpy()
+        assert c.sum() == len(keys)
+        pos = 0
+        for s_ in range(c.shape[0]):
+            for j in range(c.shape[1]):
+                seg = part[pos:pos + c[s_, j]]
+                assert (seg == ((dist.get_rank() << sub) | (bin0 + j))).all()
+                pos += c[s_, j]
+
+    def build_routed(self, t, counts, nranks, sub):
+        self.calls["build"] += 1
+        self._check_layout(t, counts, 0, nranks, sub)
+        self.routed = (nranks, sub)
+        self.r = t.numpy().copy()
+
+    def probe_routed(self, t, counts, bin0, out_r, out_s):
+        self._check_layout(t, counts, bin0, *self.routed)
+        return self.probe_tuples(t, out_r, out_s)
+
     def probe_tuples(self, t, out_r, out_s):
         self.calls["probe"] += 1
         s = t.numpy()
@@ -157,14 +199,19 @@ def _dj_worker(rank, world, port, case, outdir):
     o_r, o_s = distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
                                 replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"),
                                 n_build_global=case["NR"] if case.get("known_nr") else None,
-                                s_parts=case.get("s_parts"))
+                                s_parts=case.get("s_parts"), route_bits=case.get("route_bits"))
     nrows = ph["rows"]
     if ph["mode"] == "shuffle":
         # every output key is owned here (S.pay of the generators is the global row id)
         assert hj.calls["partition"] == 2
         full_sk = _relations(case, 0, 1)[2]
         if o_s.numel():
-            assert (_np_partition_of(full_sk[o_s.numpy()], world) == rank).all()
+            if ph.get("folded"):   # owner = the top log2(world) bits of the radix hash
+                own = _CpuJoin._rparts(full_sk[o_s.numpy()], world.bit_length() - 1) if world > 1 else 0
+                assert (np.asarray(own) == rank).all()
+            else:
+                assert (_np_partition_of(full_sk[o_s.numpy()], world) == rank).all()
+        assert ph.get("folded", False) == (case.get("route_bits", 0) > 0 and (world & (world - 1)) == 0)
     else:
         assert hj.calls["partition"] == 0 and nrows[0] == case["NR"]
     assert ph["start"].elapsed_time(ph["probed"]) >= 0.0
@@ -190,9 +237,15 @@ def _dj_worker(rank, world, port, case, outdir):
     dict(dist="pkfk", NR=7, NS=2, frac=1.0, seed=33, s_parts=5, world=2),               # empty parts
     dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=34, world=1),                    # identity exchange
     dict(dist="uniform", NR=2000, NS=2500, hi=300, seed=35, world=1, s_parts=2, capacity=700),
+    # the folded routing: rows arrive first-pass partitioned (layout checked per part)
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=36, route_bits=3),
+    dict(dist="uniform", NR=2000, NS=2600, hi=300, seed=37, route_bits=2, s_parts=3, world=4, max_rows=101),
+    dict(dist="pkfk", NR=4000, NS=6001, frac=0.9, seed=38, route_bits=4, world=3),      # 3 ranks: not folded
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=39, route_bits=5, world=1, s_parts=2, capacity=900),
 ], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
         "tiny_4ranks", "known_build_size", "known_build_size_replicate", "s_parts3", "s_parts_overflow",
-        "s_parts_empty", "one_rank", "one_rank_s_parts2"])
+        "s_parts_empty", "one_rank", "one_rank_s_parts2", "folded", "folded_4ranks_parts", "folded_3ranks_falls_back",
+        "folded_one_rank_parts"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)

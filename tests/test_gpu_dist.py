@@ -69,6 +69,72 @@ def _owner_join(hj, rk, rp, sk, sp, P):
     return outs
 
 
+def _owner_join_folded(hj, rk, rp, sk, sp, P, sub, s_parts=1):
+    """The folded routing (hj_dev_route_i64): owner and first-pass bin from
+    the radix hash; each owner's slices joined with the routed build / probe
+    (one local pass), its S in s_parts bin ranges: lists of (o_r, o_s)."""
+    F = 1 << sub
+    tr, cr = hj.route(rk, rp, P, sub)
+    ts, cs = hj.route(sk, sp, P, sub)
+    crh, csh = cr.cpu().numpy(), cs.cpu().numpy()
+    offr = np.concatenate([[0], np.cumsum(crh)])
+    offs = np.concatenate([[0], np.cumsum(csh)])
+    outs = []
+    for q in range(P):
+        hj.build_routed(tr[offr[q * F]:offr[(q + 1) * F]], cr[q * F:(q + 1) * F].view(1, F), P, sub)
+        rs, ss = [], []
+        for k in range(s_parts):
+            b0, b1 = q * F + F * k // s_parts, q * F + F * (k + 1) // s_parts
+            sq = ts[offs[b0]:offs[b1]]
+            cap = max(1, sq.shape[0])
+            for _ in range(2):
+                o_r = torch.empty(cap, dtype=torch.int64, device="cuda"); o_s = torch.empty_like(o_r)
+                m = int(hj.probe_routed(sq, cs[b0:b1].view(1, b1 - b0), b0 - q * F, o_r, o_s).item())
+                if m <= cap:
+                    break
+                cap = m
+            rs.append(o_r[:m]); ss.append(o_s[:m])
+        outs.append((torch.cat(rs), torch.cat(ss)))
+    return outs
+
+
+@pytest.mark.parametrize("P,sub,s_parts", [(1, 5, 1), (2, 4, 3), (8, 2, 2), (8, 6, 1)])
+@pytest.mark.parametrize("kind", ["pkfk", "dups"])
+def test_owner_slices_folded_vs_oracle(hj, oracle, P, sub, s_parts, kind):
+    """Folded routing: every owner's slices, routed build + routed probe in bin
+    ranges, equal the oracle's join; every slice holds only its owner's keys."""
+    if kind == "pkfk":
+        rk, rp, sk, sp = oracle.gen_pkfk_i64(70 + P + sub, 40000, 60000, 0.85)
+    else:
+        rk, rp = oracle.gen_uniform_i64(80 + P + sub, 1, 1, 900, 20000)
+        sk, sp = oracle.gen_uniform_i64(80 + P + sub, 2, 1, 900, 25000)
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    outs = _owner_join_folded(hj, d(rk), d(rp), d(sk), d(sp), P, sub, s_parts)
+    got_r = np.concatenate([o[0].cpu().numpy() for o in outs])
+    got_s = np.concatenate([o[1].cpu().numpy() for o in outs])
+    assert oracle.same_multiset(got_r, got_s, *oracle.nested_loop_i64(rk, rp, sk, sp))
+    assert hj.join_kernel in ("k_join_b", "k_join_u")
+
+
+@pytest.mark.slow
+def test_c3_eight_owner_folded_2p28(hj):
+    """C3 split over 8 owners by the folded routing (64 first-pass bins per
+    owner), each owner built and probed with one local pass."""
+    n = 1 << 28
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EED, n, n)
+    sub = hashjoin.HashJoin.route_plan(n, 8)
+    assert sub == 6
+    outs = _owner_join_folded(hj, rk, rp, sk, sp, 8, sub, s_parts=2)
+    sizes = [o[0].numel() for o in outs]
+    assert sum(sizes) == n
+    assert max(sizes) / (n / 8) < 1.01
+    o_r = torch.cat([o[0] for o in outs])
+    o_s = torch.cat([o[1] for o in outs])
+    del outs
+    assert bool((rk[o_r] == sk[o_s]).all())
+    assert torch.equal(torch.sort(o_s)[0], torch.arange(n, device="cuda"))
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("kind", ["pkfk", "dups"])
 def test_owner_slices_vs_oracle(hj, oracle, P, kind):
