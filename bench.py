@@ -201,9 +201,11 @@ def pmc_record(config, n_gpus):
     return e, f"rocprofv3 PMC, {e.get('source', '')}"
 
 
-def traffic_of(rec, names, optional=()):
+def traffic_of(rec, names, optional=(), pass_forms=None):
     """HBM bytes per launch summed over the probe phase's kernels (and those
-    of `optional` that ran)."""
+    of `optional` that ran).  pass_forms: the k_pass variants of the phase
+    (substring of the template arguments, e.g. "true, 4," for the bucketed
+    second pass); default every variant."""
     if not rec:
         return None
     ks = rec.get("kernels", {})
@@ -214,7 +216,10 @@ def traffic_of(rec, names, optional=()):
             return None
         if base == "k_pass":
             # the S side runs each k_pass variant once: sum the variants' averages
-            tot += sum(v["hbm_bytes_per_launch"] for v in k["variants"].values())
+            vs = [v for name, v in k["variants"].items() if pass_forms is None or any(f in name for f in pass_forms)]
+            if not vs:
+                return None
+            tot += sum(v["hbm_bytes_per_launch"] for v in vs)
         else:
             tot += k["hbm_bytes_per_launch"]
     return int(tot)
@@ -347,7 +352,7 @@ def main():
                 phases["probe"] += ev["built"].elapsed_time(ev["probed"])
             last["m"] = o_r.numel()
             last["rows"] = ev["rows"]
-            last["mode"] = ev["mode"]
+            last["mode"] = ev["mode"] + (", folded routing" if ev.get("folded") else "")
 
     for _ in range(a.warmup):
         step(False)
@@ -403,7 +408,7 @@ def main():
         nr_loc, ns_loc = last["rows"]
         probe_bytes = ns_loc * (K + SLOT) + m_local * PAIR
         read_bytes = ns_loc * (K + SLOT)
-    rec, traffic_note = pmc_record(a.config, world)
+    rec, traffic_note = pmc_record(a.config + ("-dist" if use_dist else ""), world)
     info = hashjoin.device_info(local)
 
     def frac(b, t_ms, peak=HBM_PEAK_GBS):
@@ -417,7 +422,11 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": frac(probe_bytes, probe_ms),
-        "traffic": traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS) if (strategy == "radix" and not use_dist) else None,
+        # (the distributed path's probe phase: the routed S's one local pass,
+        # the bucketed-input k_pass, + the join; routing is its own phase)
+        "traffic": (traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS,
+                               pass_forms=("<true, 4,", "<false, 4,") if use_dist else None)
+                    if strategy == "radix" and (not use_dist or world == 1) else None),
         "traffic_source": traffic_note,
         "algorithmic_bytes": probe_bytes,
         "bytes_per_probe_row": round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2),
