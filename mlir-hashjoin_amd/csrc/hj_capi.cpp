@@ -168,6 +168,11 @@ struct hj_ctx {
     bool join_ran = false, join_wide = false, join_stream = false;
     bool routed = false;   // the current build came from hj_dev_build_routed_i64 (plan.skip owner bits)
     hipStream_t join_st = nullptr;
+    // ... and its R view and partition count, for the on-demand repeat check
+    // (hj_ctx_build_has_duplicates); join_checked: that check ran for it
+    hj::BucketSet join_r{};
+    int join_nparts = -1;
+    bool join_checked = false;
 };
 
 namespace {
@@ -422,6 +427,9 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         c->join_wide = wide;
         c->join_stream = stream;
         c->join_st = st;
+        c->join_r = bucket_set(c->rset);
+        c->join_nparts = -1;
+        c->join_checked = false;
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
@@ -1062,6 +1070,19 @@ int hj_ctx_build_has_duplicates(hj_ctx *c) {
     unsigned long long v = 0;
     HJ_HIP(hipDeviceSynchronize());
     HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
+    if (!v && c->join_ran && !c->join_checked && c->join_wide && !c->join_stream) {
+        // k_join_b flags only the repeats its probe rows met: the rest of the
+        // answer, once per join (its items' work map is still resident)
+        unsigned long long smp[2] = {0, 0};
+        HJ_HIP(hipMemcpy(smp, c->meta + 2, sizeof(smp), hipMemcpyDeviceToHost));
+        if (hj::join_kernel_choice(c->join_wide, c->join_stream, smp[0], smp[1]) == HJ_JOIN_KERNEL_BUCKETED) {
+            HJ_HIP(hj::radix_detect(c->plan, c->join_r, (const unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1,
+                                    c->meta + 2, c->join_nparts, c->join_st));
+            HJ_HIP(hipDeviceSynchronize());
+            HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
+        }
+        c->join_checked = true;
+    }
     return v ? 1 : 0;
 }
 
@@ -1314,6 +1335,9 @@ int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->join_wide = true;
     c->join_stream = stream_shape;
     c->join_st = st;
+    c->join_r = r;
+    c->join_nparts = nbins << c->plan.bits[1];
+    c->join_checked = false;
     record(c, kEvProbe1, st);
     c->rec[2] = c->timing;
     c->rec_mid = c->timing;

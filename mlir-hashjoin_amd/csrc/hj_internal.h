@@ -221,6 +221,12 @@ hipError_t radix_partition_routed(const void *tuples, long long n, const unsigne
 // the caller).  Deterministic for given data.
 hipError_t radix_sample(bool wide, const RadixPlan &pl, const BucketSet &r, unsigned long long *sample,
                         hipStream_t st);
+// The exact "build keys repeat" answer for the items of the last radix_join
+// (work_start / desc as it left them, same r view and nparts) that k_join_b
+// joined: its DETECT build, setting *dup_flag.  (k_join_b only flags repeats a
+// probe row met; the other join kernels answer exactly during the join.)
+hipError_t radix_detect(const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
+                        unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st);
 // HJ_JOIN_KERNEL_* of the radix join for this shape and sample (host mirror
 // of the device-side choice)
 int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned long long repeats);

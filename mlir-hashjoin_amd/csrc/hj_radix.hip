@@ -1809,22 +1809,31 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 //            < 4: the slot; else the next bucket, and so on -- rare at load
 //            0.5), then plain stores of key and payload; no EMPTY marker,
 //            no table fill (the counts say which slots are live)
-//   dups   = every row ORs a 1-of-32 fingerprint of its key into its home
-//            bucket's signature (returning LDS or); a row that finds its
-//            bit already set is a suspect, and after the build each suspect
-//            (~3 % of the rows when keys are unique) looks for another live
-//            slot holding its key along its chain.  Exact: of c copies of a
-//            key all but the first to OR its bit are suspects and each finds
-//            a twin; a suspect without a twin is a fingerprint collision.
-//   probe  = the home bucket's count and its 4 keys (two 16-B reads), all
-//            rows' reads in flight together; a bucket whose count exceeds 4
-//            had a row pass it, so the walk goes on to the next bucket.
-// A bucket's count keeps growing as rows pass it (<= 4096: no overflow).
-// The product launches it for int64 rows only (i32 rows keep k_join_u, where
-// their many-repeat deferral to k_join_grp lives).  ABL (micro/join3_micro.hip
-// ablations only; 0 in the product): bit 0 no suspect checks, bit 1 no
-// fingerprints (timing only).
-template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, int ABL = 0>
+//            A row that finds its home bucket full ORs its key's overflow bit
+//            (1 of 16, from hash bits below the bucket's) into the home
+//            bucket's word before walking on.
+//   probe  = the home bucket's word and its 4 keys (two 16-B reads), all
+//            rows' reads in flight together: the first match and the number
+//            of matching slots there.  Only a key whose overflow bit is set
+//            in its home word can have copies further on; those rows walk the
+//            rest of the chain (on while a bucket's count exceeds 4: a row
+//            passed it), counting.  A row with more than one matching slot is
+//            a multi row: its pairs go out by a chain walk.
+// Repeated build keys thus cost nothing when no probe row meets one: no
+// build-time repeat check (the suspect walks the kernel ran until round 3
+// cost C3 0.2 ms, C1-ref 0.26 ms: the walks sat between the build barrier
+// and the first ballot barrier).  The context's "build keys repeat" flag is
+// set by a probe row that met a repeated key; the exact answer for build
+// keys no probe row met comes from DETECT (hj_ctx_build_has_duplicates, on
+// demand): the same build, with every row ORing a 1-of-32 signature of its
+// key into its home bucket's signature word (returning LDS or); a row that
+// finds its bit already set is a suspect and looks for another live slot
+// holding its key along its chain.  Exact: of c copies of a key all but the
+// first to OR its bit are suspects and each finds a twin.
+// A bucket's count keeps growing as rows pass it (<= 4096 < 2^16).  The
+// product launches it for int64 rows only (i32 rows keep k_join_u, where
+// their many-repeat deferral to k_join_grp lives).
+template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false>
 __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
@@ -1840,19 +1849,20 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     constexpr unsigned rmax_rows = (unsigned)(TS * 3 / 4);
     static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
     constexpr unsigned kNone = 0xFFFFFFFFu, kMulti = 0xFFFFFFFEu;
+    // a bucket's word: its count (rows stored in it or passed it, <= 4096) in
+    // the low half, the overflow bits of the keys stored past it in the high
+    constexpr unsigned kCntMask = 0xFFFFu;
     __shared__ __attribute__((aligned(16))) u64 tkey[TS];
     __shared__ __attribute__((aligned(16))) u64 tpay[WIDE ? TS : 2];
     __shared__ __attribute__((aligned(16))) unsigned bcnt[NB];
-    __shared__ __attribute__((aligned(16))) unsigned bsig[NB];   // home bucket: OR of its rows' key fingerprints
+    // (DETECT) per home bucket the OR of its rows' 1-of-32 key signatures,
+    // and the suspect slots: slot | home bucket << 16
     constexpr unsigned kSusCap = 512;
-    __shared__ unsigned sus[kSusCap];   // suspect slots: slot | home bucket << 16
+    __shared__ __attribute__((aligned(16))) unsigned bsig[DETECT ? NB : 4];
+    __shared__ unsigned sus[DETECT ? kSusCap : 1];
     __shared__ u64 s_base;
     __shared__ __attribute__((aligned(16))) unsigned s_ctl[4];   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
     unsigned &s_bad = s_ctl[0], &s_dup = s_ctl[1], &s_rows = s_ctl[2], &s_nsus = s_ctl[3];
-    // slots whose key is held by another live slot too (set by the suspects'
-    // chain checks): a probe row whose first match is marked takes the
-    // multi-match path
-    __shared__ __attribute__((aligned(16))) unsigned sdup[TS / 32];
     // per (row slot, wave) ballot counts, then per wave the multi rows' pairs
     __shared__ unsigned s_cw[SI * NW + NW];
     __shared__ unsigned s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
@@ -1892,26 +1902,32 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
         }
         return ok;
     };
-    // live keys of bucket b: its count (capped at BW) and its 4 slots
+    // (a key's overflow bit: 1 of the 16 high bits of its home bucket's word)
+    auto ovf_bit = [&](u64 key) { return 1u << (16u + ((unsigned)(rhash(key) >> fsh) & 15u)); };
+    // live keys of bucket b: its count (capped at BW) and its 4 slots; returns
+    // the bucket's word (its overflow bits)
     auto read_bucket = [&](unsigned b, unsigned &c, u64 *k4) {
-        c = bcnt[b];
+        const unsigned raw = bcnt[b];
+        c = raw & kCntMask;
         const ulonglong2 q0 = ((const ulonglong2 *)tkey)[b * 2], q1 = ((const ulonglong2 *)tkey)[b * 2 + 1];
         k4[0] = q0.x;
         k4[1] = q0.y;
         k4[2] = q1.x;
         k4[3] = q1.y;
+        return raw;
     };
     T sv_[SI], rv_[RI];
     u64 er[RI], es[SI];
     ItemDesc it = sload(a.desc + w);
     ents(a.r_runs, it.r_lo, it.r_hi, er, RI);
-    ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    // (DETECT reads no probe rows)
+    if (!DETECT) ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
     while (true) {
         const bool fits = it.r_hi - it.r_lo <= (u64)rmax;
         unsigned rok = 0, sok = 0;
         if (fits) {
             rok = rows_of(rrows, er, rv_, RI);
-            sok = rows_of(srows, es, sv_, SI);
+            if (!DETECT) sok = rows_of(srows, es, sv_, SI);
         }
         const bool more = w + gridDim.x < total;
         u64 ner[RI], nes[SI];
@@ -1919,10 +1935,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
         if (more) {
             nx = sload(a.desc + w + gridDim.x);
             ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
-            ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+            if (!DETECT) ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
         }
         if (!fits) {
-            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            if (!DETECT && threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
         } else {
             // (zeros from the item's descriptor -- r_lo < 2^63 -- or the
             // compiler keeps a constant zero quad live across the loop and
@@ -1931,19 +1947,18 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             const uint4 z4 = make_uint4(z, z, z, z);
             // (thread 0 clears the control words: it is also the one that
             // reads the previous item's s_dup after the item's last barrier)
-            static_assert(NB / 2 + TS / 128 <= NT, "one 16-B clear per thread: counts, signatures, repeat marks");
+            static_assert(NB / 2 <= NT, "one 16-B clear per thread: counts, signatures");
             // (the index carries z too: a loop-invariant clear address was
             // hoisted out of the item loop and spilled)
             const unsigned ci = threadIdx.x + z;
             if (ci < NB / 4) ((uint4 *)bcnt)[ci] = z4;
-            else if (ci < NB / 2) ((uint4 *)bsig)[ci - NB / 4] = z4;
-            else if (ci < NB / 2 + TS / 128) ((uint4 *)sdup)[ci - NB / 2] = z4;
+            else if (DETECT && ci < NB / 2) ((uint4 *)bsig)[ci - NB / 4] = z4;
             if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
             __syncthreads();
             // ---- build: every row's rank add issued before any is used
             bool bad = false;
             for (u64 r0 = it.r_lo;;) {
-                unsigned bb[RI], rk[RI], susm = 0u;   // susm bit i: row i's fingerprint was set
+                unsigned bb[RI], rk[RI], susm = 0u;   // (DETECT) susm bit i: row i's signature bit was set
 #pragma unroll
                 for (int i = 0; i < RI; ++i) {
                     const u64 key = R::key(rv_[i]);
@@ -1954,9 +1969,11 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                     }
                     const u64 hh = rhash(key);
                     bb[i] = (unsigned)(hh >> bsh) & kBMask;
-                    rk[i] = act ? atomicAdd(&bcnt[bb[i]], 1u) : 0u;
-                    const unsigned fp = 1u << ((unsigned)(hh >> fsh) & 31u);
-                    if (!(ABL & 2) && act && (atomicOr(&bsig[bb[i]], fp) & fp)) susm |= 1u << i;
+                    rk[i] = act ? atomicAdd(&bcnt[bb[i]], 1u) & kCntMask : 0u;
+                    if constexpr (DETECT) {
+                        const unsigned fp = 1u << ((unsigned)(hh >> fsh) & 31u);
+                        if (act && (atomicOr(&bsig[bb[i]], fp) & fp)) susm |= 1u << i;
+                    }
                     if (!act) rok &= ~(1u << i);
                 }
                 {
@@ -1969,12 +1986,16 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                 for (int i = 0; i < RI; ++i) {
                     if (!((rok >> i) & 1u)) continue;
                     const unsigned home = bb[i];
+                    // a row stored past its home bucket leaves its key's
+                    // overflow bit there: the probe walks on past a home bucket
+                    // only for a key whose bit is set
+                    if (!DETECT && rk[i] >= (unsigned)BW) atomicOr(&bcnt[home], ovf_bit(R::key(rv_[i])));
                     // a full bucket: the next one (the table never fills:
                     // <= rmax_rows rows, else the item is deferred and a
                     // full table's walk is cut at NB buckets)
                     for (unsigned g = 0; rk[i] >= (unsigned)BW && g < (unsigned)NB; ++g) {
                         bb[i] = (bb[i] + 1u) & kBMask;
-                        rk[i] = atomicAdd(&bcnt[bb[i]], 1u);
+                        rk[i] = atomicAdd(&bcnt[bb[i]], 1u) & kCntMask;
                     }
                     if (rk[i] >= (unsigned)BW) {   // (only past rmax_rows: deferred)
                         s_bad = 1u;
@@ -1987,10 +2008,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                     } else {
                         tkey[slot] = rv_[i];
                     }
-                    if ((susm >> i) & 1u) {
+                    if (DETECT && ((susm >> i) & 1u)) {
                         const unsigned q = atomicAdd(&s_nsus, 1u);
                         if (q < kSusCap) sus[q] = slot | home << 16;
-                        else s_bad = 1u;   // (this many: k_join)
                     }
                 }
                 r0 += rb;
@@ -2001,47 +2021,52 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             if (bad) s_bad = 1u;
             __syncthreads();
             if (s_bad) {
-                if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
-            } else {
-            // ---- repeated build keys: each suspect walks its chain (home
-            // bucket, then on while a bucket's count says a row passed it) and,
-            // when another live slot holds its key, marks EVERY live slot with
-            // that key, itself included.  Of c copies of a key all but the
-            // first to OR its fingerprint are suspects, so every copy gets
-            // marked.  The verdict (s_dup) is read after the first sub-chunk's
-            // ballot barrier: the walks overlap the probe's reads.
-            {
-                unsigned ndup = 0;
+                // (DETECT: the item went to k_join, whose build flagged repeats)
+                if (!DETECT && threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            } else if constexpr (DETECT) {
+                // ---- the exact "build keys repeat" answer: each suspect walks
+                // its chain (home bucket, then on while a bucket's count says a
+                // row passed it) for another live slot holding its key.  Of c
+                // copies of a key all but the first to OR its signature bit are
+                // suspects and each finds a twin; a suspect without a twin is a
+                // signature collision.
+                // (more suspects than sus[] holds: every live slot checks)
+                bool twin = false;
                 const unsigned nsus = s_nsus;
-                for (unsigned q = threadIdx.x; q < nsus && !(ABL & 1); q += NT) {
-                    const unsigned e = sus[q], slot = e & 0xFFFFu;
-                    const u64 key = kof(tkey[slot]);
-                    unsigned h = e >> 16;
-                    bool twin = false;
-                    // one walk: every other live slot with the key is marked as
-                    // found, the suspect's own slot after the walk if any was
+                const bool all = nsus > kSusCap;
+                for (unsigned q = threadIdx.x; q < (all ? (unsigned)TS : nsus) && !twin; q += NT) {
+                    unsigned slot, h;
+                    u64 key;
+                    if (all) {
+                        const unsigned lc = bcnt[q / BW] & kCntMask;
+                        if (q % BW >= (lc < (unsigned)BW ? lc : (unsigned)BW)) continue;
+                        slot = q;
+                        key = kof(tkey[slot]);
+                        h = bucket(key);
+                    } else {
+                        const unsigned e = sus[q];
+                        slot = e & 0xFFFFu;
+                        key = kof(tkey[slot]);
+                        h = e >> 16;
+                    }
                     for (unsigned g = 0; g < (unsigned)NB; ++g) {
                         unsigned c;
                         u64 k4[BW];
                         read_bucket(h, c, k4);
 #pragma unroll
-                        for (int j = 0; j < BW; ++j) {
-                            const unsigned sl = h * BW + (unsigned)j;
-                            if ((unsigned)j < c && sl != slot && kof(k4[j]) == key) {
-                                atomicOr(&sdup[sl >> 5], 1u << (sl & 31u));
-                                twin = true;
-                            }
-                        }
+                        for (int j = 0; j < BW; ++j)
+                            twin |= (unsigned)j < c && h * BW + (unsigned)j != slot && kof(k4[j]) == key;
                         if (c <= (unsigned)BW) break;
                         h = (h + 1u) & kBMask;
                     }
-                    if (twin) {
-                        ++ndup;
-                        atomicOr(&sdup[slot >> 5], 1u << (slot & 31u));
-                    }
                 }
-                if (ndup) atomicAdd(&s_dup, ndup);
-            }
+                if (twin) s_dup = 1u;
+                __syncthreads();
+                if (threadIdx.x == 0 && s_dup && !dup_sent) {
+                    __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    dup_sent = true;
+                }
+            } else {
             // the matches of `key` along its chain: counted, or written from pos
             auto chain = [&](u64 key, bool wr, u64 pos, PT spay) {
                 unsigned h = bucket(key), cnt = 0;
@@ -2064,7 +2089,6 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                 }
                 return cnt;
             };
-            bool known = false, dups = false;
                 for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
                     if (sb != it.s_lo) {
                         ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
@@ -2074,8 +2098,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
 #pragma unroll
                     for (int i = 0; i < SI; ++i)
                         if (((sok >> i) & 1u) && !(WIDE && R::key(sv_[i]) == kEmptyKey64)) pm |= 1u << i;
-                    // every row's first match: the home buckets of all rows
-                    // read before any is resolved
+                    // every row's home bucket, all rows' reads in flight
+                    // together: its first match there and how many slots match
+                    // (cb: the bucket's count | matching slots << 16)
                     unsigned m[SI], hb[SI], cb[SI];
 #pragma unroll
                     for (int i = 0; i < SI; ++i) {
@@ -2084,69 +2109,69 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         cb[i] = 0u;
                         if ((pm >> i) & 1u) {
                             u64 k4[BW];
-                            read_bucket(hb[i], cb[i], k4);
                             const u64 key = R::key(sv_[i]);
+                            unsigned c, nm = 0u;
+                            const unsigned ov = read_bucket(hb[i], c, k4);
 #pragma unroll
-                            for (int j = BW - 1; j >= 0; --j)
-                                if ((unsigned)j < cb[i] && kof(k4[j]) == key) m[i] = hb[i] * BW + j;
+                            for (int j = BW - 1; j >= 0; --j) {
+                                if ((unsigned)j < c && kof(k4[j]) == key) {
+                                    m[i] = hb[i] * BW + j;
+                                    ++nm;
+                                }
+                            }
+                            // no copy of the key went past its home bucket:
+                            // the home bucket held all of them
+                            cb[i] = (ov & ovf_bit(key) ? c : 0u) | nm << 16;
                         }
                     }
-                    // rows whose home bucket was passed by a full one's rows
+                    // keys with a copy past the home bucket (or a collision of
+                    // overflow bits): the rest of the chain -- on while a
+                    // bucket's count says a row passed it
 #pragma unroll
                     for (int i = 0; i < SI; ++i) {
-                        if (!((pm >> i) & 1u)) continue;
                         const u64 key = R::key(sv_[i]);
-                        unsigned h = hb[i], c = cb[i];
-                        for (unsigned g = 0; m[i] == kNone && c > (unsigned)BW && g < (unsigned)NB; ++g) {
+                        unsigned h = hb[i], c = cb[i] & kCntMask;
+                        for (unsigned g = 0; c > (unsigned)BW && g < (unsigned)NB; ++g) {
                             h = (h + 1u) & kBMask;
                             u64 k4[BW];
                             read_bucket(h, c, k4);
+                            unsigned f = kNone;
 #pragma unroll
-                            for (int j = BW - 1; j >= 0; --j)
-                                if ((unsigned)j < c && kof(k4[j]) == key) m[i] = h * BW + j;
+                            for (int j = BW - 1; j >= 0; --j) {
+                                if ((unsigned)j < c && kof(k4[j]) == key) {
+                                    f = h * BW + j;
+                                    cb[i] += 1u << 16;
+                                }
+                            }
+                            if (m[i] == kNone) m[i] = f;
                         }
                     }
                     const int wv = threadIdx.x >> 6;
-                    // multi rows (first match on a marked slot; m = kMulti): all
-                    // their pairs go out by a chain walk from a wave-prefix
+                    // multi rows (m = kMulti: more than one slot holds the key):
+                    // all their pairs go out by a chain walk from a wave-prefix
                     // position; the others by ballot compaction
                     unsigned cntm = 0u;
-                    auto split = [&]() {
 #pragma unroll
-                        for (int i = 0; i < SI; ++i) {
-                            if (m[i] != kNone && ((sdup[m[i] >> 5] >> (m[i] & 31u)) & 1u)) {
-                                m[i] = kMulti;
-                                cntm += chain(R::key(sv_[i]), false, 0, (PT)0);
-                            }
-                        }
-                    };
-                    auto ballots = [&]() {
-#pragma unroll
-                        for (int i = 0; i < SI; ++i) {
-                            const u64 bal = __ballot(m[i] < kMulti);
-                            if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
-                        }
-                        const unsigned xm = wave_incl_add(cntm);
-                        if (dups) s_mpre[threadIdx.x] = xm - cntm;
-                        if (lane == 63) s_cw[SI * NW + wv] = xm;
-                    };
-                    if (dups) split();
-                    ballots();
-                    __syncthreads();
-                    if (!known) {
-                        known = true;
-                        dups = s_dup != 0u;
-                        if (dups) {
-                            if (!dup_sent) {   // once per workgroup (k_join)
-                                if (threadIdx.x == 0)
-                                    __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                dup_sent = true;
-                            }
-                            split();     // (the marks are complete now)
-                            ballots();   // (s_cw: nothing reads it before this barrier)
-                            __syncthreads();
+                    for (int i = 0; i < SI; ++i) {
+                        if ((cb[i] >> 16) > 1u) {
+                            m[i] = kMulti;
+                            cntm += cb[i] >> 16;
                         }
                     }
+#pragma unroll
+                    for (int i = 0; i < SI; ++i) {
+                        const u64 bal = __ballot(m[i] < kMulti);
+                        if (lane == 0) s_cw[i * NW + wv] = (unsigned)__popcll(bal);
+                    }
+                    {
+                        const unsigned xm = wave_incl_add(cntm);
+                        if (cntm) {
+                            s_mpre[threadIdx.x] = xm - cntm;
+                            s_dup = 1u;
+                        }
+                        if (lane == 63) s_cw[SI * NW + wv] = xm;
+                    }
+                    __syncthreads();
                     if (wv == 0) {
                         constexpr int NE = SI * NW + NW;
                         constexpr int K = (NE + 63) / 64;
@@ -2178,6 +2203,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                                 if constexpr (WRITE) s_base = atomicAdd(a.counter, (u64)x);
                                 else atomicAdd(a.counter, (u64)x);
                             }
+                            // a probe row met a repeated build key: the
+                            // context's repeat flag, once per workgroup (k_join)
+                            if (s_dup && !dup_sent) {
+                                __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                dup_sent = true;
+                            }
                         }
                     }
                     if constexpr (WRITE) {
@@ -2193,7 +2224,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                                 st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
                             }
                         }
-                        if (dups) {
+                        if (cntm) {
                             u64 pos = s_base + s_cw[SI * NW + wv] + s_mpre[threadIdx.x];
 #pragma unroll
                             for (int i = 0; i < SI; ++i)
@@ -2614,11 +2645,35 @@ __global__ __launch_bounds__(1024) void k_slot_hist(PassArgs a, u64 *hist) {
     const unsigned t0 = (unsigned)((u64)blockIdx.x * T_ / gridDim.x);
     const unsigned t1 = (unsigned)((u64)(blockIdx.x + 1) * T_ / gridDim.x);
     const u64 r0 = (u64)t0 * kTile, r1 = (u64)t1 * kTile < a.n ? (u64)t1 * kTile : a.n;
-    for (u64 r = r0 + threadIdx.x; r < r1; r += 1024) {
-        u64 key;
-        if constexpr (FORM == kCols64) key = ((const u64 *)a.in.key)[r];
-        else key = R::key(((const typename R::T *)a.in.key)[r]);
-        atomicAdd(&c[(unsigned)(rhash(key) >> a.shift) & (F - 1)], 1u);
+    // 8 keys per thread in flight per step (a tile = 4096 rows = 1024 x 4:
+    // two tiles per step); key columns as 16-B pairs when aligned
+    constexpr int U = 8;
+    auto key_at = [&](u64 r) -> u64 {
+        if constexpr (FORM == kCols64) return ((const u64 *)a.in.key)[r];
+        else return R::key(((const typename R::T *)a.in.key)[r]);
+    };
+    for (u64 rb = r0; rb < r1; rb += (u64)U * 1024) {
+        u64 k[U];
+        bool v[U];
+        if (FORM == kCols64 && (((uintptr_t)a.in.key) & 15) == 0 && rb + (u64)U * 1024 <= r1) {
+#pragma unroll
+            for (int i = 0; i < U / 2; ++i) {
+                const ulonglong2 k2 = ((const ulonglong2 *)((const u64 *)a.in.key + rb))[(u64)i * 1024 + threadIdx.x];
+                k[2 * i] = k2.x;
+                k[2 * i + 1] = k2.y;
+                v[2 * i] = v[2 * i + 1] = true;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < U; ++i) {
+                const u64 r = rb + (u64)i * 1024 + threadIdx.x;
+                v[i] = r < r1;
+                k[i] = v[i] ? key_at(r) : 0ull;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < U; ++i)
+            if (v[i]) atomicAdd(&c[(unsigned)(rhash(k[i]) >> a.shift) & (F - 1)], 1u);
     }
     __syncthreads();
     for (unsigned b = threadIdx.x; b < F; b += 1024) hist[(u64)b * gridDim.x + blockIdx.x] = c[b];
@@ -2951,6 +3006,26 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                (k_join<false, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), 512);
 #undef HJ_WR
 #undef HJ_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t radix_detect(const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
+                        unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st) {
+    // over the last join's items (work map and descriptors still resident):
+    // the items k_join_b built -- the others' kernels answered during the join
+    JoinArgs a{};
+    a.r = r.rows;
+    a.r_runs = r.runs;
+    a.r_rstart = r.rstart;
+    a.P = nparts >= 0 ? nparts : 1 << pl.total_bits;
+    a.work_start = work_start;
+    a.desc = (const ItemDesc *)desc;
+    a.tshift = 64 - pl.skip - pl.total_bits - kTableLog;
+    a.dup_flag = dup_flag;
+    a.sample = sample;
+    a.modes = kModeUnique | kModeSome;
+    hipLaunchKernelGGL((k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS, true>), dim3(2 * cu_count()),
+                       dim3(kFastNT), 0, st, a);
     return hipGetLastError();
 }
 

@@ -150,8 +150,7 @@ int body(int lg) {
     }
     {
         run("k_join_b", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6>), dim3(2 * cus), dim3(768), 0, 0, a); });
-        run("k_join_b, no suspect checks", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6, 1>), dim3(2 * cus), dim3(768), 0, 0, a); });
-        run("k_join_b, no signatures", [&] { hipLaunchKernelGGL((k_join_b<W, true, 768, 3, 3, 6, 2>), dim3(2 * cus), dim3(768), 0, 0, a); });
+        run("k_join_b DETECT (repeat check only)", [&] { hipLaunchKernelGGL((k_join_b<W, false, 768, 3, 3, 6, true>), dim3(2 * cus), dim3(768), 0, 0, a); });
     }
     UA(1, "product shape, no cursor atomic");
     UA(2, "product shape, no output stores");

@@ -374,20 +374,26 @@ def test_radix_probe_heavy_stream_shape(hj, oracle, dist):
 
 
 @pytest.mark.parametrize("rows,bits", [(200000, 7), (180000, 6)])
-@pytest.mark.parametrize("dups", ["none", "one", "hot"])
+@pytest.mark.parametrize("dups", ["none", "one", "hot", "unprobed"])
 def test_radix_bucketed_table_repeat_detection(hj, oracle, rows, bits, dups):
-    """The wide fast join's bucketed table (k_join_b): repeated build keys
-    are found by fingerprint suspects + a chain check, so the answer must be
-    exact -- no repeat among unique keys at ~1500 and ~2800 rows per
-    partition (the second crowds buckets into overflow chains), one repeated
-    pair, and one key 40 times (its copies fill its home bucket and spill
-    over)."""
+    """The wide fast join's bucketed table (k_join_b): a probe row that meets
+    a repeated build key flags the repeat during the join, and the rest of the
+    exact answer comes from the on-demand check (k_join_b DETECT: signature
+    suspects + a chain check) -- no repeat among unique keys at ~1500 and
+    ~2800 rows per partition (the second crowds buckets into overflow
+    chains), one repeated pair, one key 40 times (its copies fill its home
+    bucket and spill over), and repeats no probe row meets."""
     rk, rp, sk, sp = oracle.gen_pkfk_i64(rows + bits, rows, rows, 0.8)
     rk = rk.copy()
     if dups == "one":
         rk[7] = rk[12345]
     elif dups == "hot":
         rk[100:140] = rk[99]
+    elif dups == "unprobed":
+        rk[7] = rk[12345]
+        rk[100:140] = rk[99]
+        sk = sk.copy()
+        sk[np.isin(sk, rk[[7, 99]])] = -5   # (the oracle joins it like any key)
     o = run(hj, rk, rp, sk, sp, bits)
     assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
     assert hj.has_duplicates() == (dups != "none")
