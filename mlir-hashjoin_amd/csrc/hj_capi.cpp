@@ -1070,13 +1070,13 @@ int hj_ctx_build_has_duplicates(hj_ctx *c) {
     unsigned long long v = 0;
     HJ_HIP(hipDeviceSynchronize());
     HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
-    if (!v && c->join_ran && !c->join_checked && c->join_wide && !c->join_stream) {
+    if (!v && c->join_ran && !c->join_checked) {
         // k_join_b flags only the repeats its probe rows met: the rest of the
         // answer, once per join (its items' work map is still resident)
         unsigned long long smp[2] = {0, 0};
         HJ_HIP(hipMemcpy(smp, c->meta + 2, sizeof(smp), hipMemcpyDeviceToHost));
         if (hj::join_kernel_choice(c->join_wide, c->join_stream, smp[0], smp[1]) == HJ_JOIN_KERNEL_BUCKETED) {
-            HJ_HIP(hj::radix_detect(c->plan, c->join_r, (const unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1,
+            HJ_HIP(hj::radix_detect(c->join_wide, c->plan, c->join_r, (const unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1,
                                     c->meta + 2, c->join_nparts, c->join_st));
             HJ_HIP(hipDeviceSynchronize());
             HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));

@@ -225,7 +225,7 @@ hipError_t radix_sample(bool wide, const RadixPlan &pl, const BucketSet &r, unsi
 // (work_start / desc as it left them, same r view and nparts) that k_join_b
 // joined: its DETECT build, setting *dup_flag.  (k_join_b only flags repeats a
 // probe row met; the other join kernels answer exactly during the join.)
-hipError_t radix_detect(const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
+hipError_t radix_detect(bool wide, const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
                         unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st);
 // HJ_JOIN_KERNEL_* of the radix join for this shape and sample (host mirror
 // of the device-side choice)

@@ -1831,8 +1831,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 // holding its key along its chain.  Exact: of c copies of a key all but the
 // first to OR its bit are suspects and each finds a twin.
 // A bucket's count keeps growing as rows pass it (<= 4096 < 2^16).  The
-// product launches it for int64 rows only (i32 rows keep k_join_u, where
-// their many-repeat deferral to k_join_grp lives).
+// i32 rows keep keys and row ids apart (a bucket's keys are one 16-B read);
+// an item whose probe rows would write many pairs per row (the reference's
+// keys in [1, 100k]) goes to k_join_grp before anything of it is written.
 template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false>
 __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     typedef Row<WIDE> R;
@@ -1880,7 +1881,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     const unsigned bsh = a.tshift + 2u;
     const unsigned fsh = a.tshift - 5u;   // (a.tshift >= 28: 64 - <= 24 partition bits - 12)
     auto bucket = [&](u64 key) { return (unsigned)(rhash(key) >> bsh) & kBMask; };
-    auto kof = [&](u64 e) { return WIDE ? e : (e >> 32); };
+    // i32 rows: the table's 32 KiB hold the keys (tkn) and, apart, the row
+    // ids (tidn): a bucket's 4 keys are one 16-B read
+    unsigned *const tkn = (unsigned *)tkey;
+    unsigned *const tidn = tkn + TS;
+    auto key_at = [&](unsigned slot) -> u64 { return WIDE ? tkey[slot] : (u64)tkn[slot]; };
+    auto pay_at = [&](unsigned slot) -> PT { return WIDE ? (PT)tpay[slot] : (PT)tidn[slot]; };
     const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
     const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
     const int lane = threadIdx.x & 63;
@@ -1909,11 +1915,19 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     auto read_bucket = [&](unsigned b, unsigned &c, u64 *k4) {
         const unsigned raw = bcnt[b];
         c = raw & kCntMask;
-        const ulonglong2 q0 = ((const ulonglong2 *)tkey)[b * 2], q1 = ((const ulonglong2 *)tkey)[b * 2 + 1];
-        k4[0] = q0.x;
-        k4[1] = q0.y;
-        k4[2] = q1.x;
-        k4[3] = q1.y;
+        if constexpr (WIDE) {
+            const ulonglong2 q0 = ((const ulonglong2 *)tkey)[b * 2], q1 = ((const ulonglong2 *)tkey)[b * 2 + 1];
+            k4[0] = q0.x;
+            k4[1] = q0.y;
+            k4[2] = q1.x;
+            k4[3] = q1.y;
+        } else {
+            const uint4 q = ((const uint4 *)tkn)[b];
+            k4[0] = q.x;
+            k4[1] = q.y;
+            k4[2] = q.z;
+            k4[3] = q.w;
+        }
         return raw;
     };
     T sv_[SI], rv_[RI];
@@ -2006,7 +2020,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         tkey[slot] = R::key(rv_[i]);
                         tpay[slot] = R::pay(rv_[i]);
                     } else {
-                        tkey[slot] = rv_[i];
+                        tkn[slot] = (unsigned)R::key(rv_[i]);
+                        tidn[slot] = (unsigned)R::pay(rv_[i]);
                     }
                     if (DETECT && ((susm >> i) & 1u)) {
                         const unsigned q = atomicAdd(&s_nsus, 1u);
@@ -2041,12 +2056,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         const unsigned lc = bcnt[q / BW] & kCntMask;
                         if (q % BW >= (lc < (unsigned)BW ? lc : (unsigned)BW)) continue;
                         slot = q;
-                        key = kof(tkey[slot]);
+                        key = key_at(slot);
                         h = bucket(key);
                     } else {
                         const unsigned e = sus[q];
                         slot = e & 0xFFFFu;
-                        key = kof(tkey[slot]);
+                        key = key_at(slot);
                         h = e >> 16;
                     }
                     for (unsigned g = 0; g < (unsigned)NB; ++g) {
@@ -2055,7 +2070,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                         read_bucket(h, c, k4);
 #pragma unroll
                         for (int j = 0; j < BW; ++j)
-                            twin |= (unsigned)j < c && h * BW + (unsigned)j != slot && kof(k4[j]) == key;
+                            twin |= (unsigned)j < c && h * BW + (unsigned)j != slot && k4[j] == key;
                         if (c <= (unsigned)BW) break;
                         h = (h + 1u) & kBMask;
                     }
@@ -2076,9 +2091,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                     read_bucket(h, c, k4);
 #pragma unroll
                     for (int j = 0; j < BW; ++j) {
-                        if ((unsigned)j < c && kof(k4[j]) == key) {
+                        if ((unsigned)j < c && k4[j] == key) {
                             if (WRITE && wr && pos + cnt < (u64)a.cap) {
-                                orr[pos + cnt] = WIDE ? (PT)tpay[h * BW + j] : (PT)(k4[j] & 0xffffffffull);
+                                orr[pos + cnt] = pay_at(h * BW + j);
                                 oss[pos + cnt] = spay;
                             }
                             ++cnt;
@@ -2114,7 +2129,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                             const unsigned ov = read_bucket(hb[i], c, k4);
 #pragma unroll
                             for (int j = BW - 1; j >= 0; --j) {
-                                if ((unsigned)j < c && kof(k4[j]) == key) {
+                                if ((unsigned)j < c && k4[j] == key) {
                                     m[i] = hb[i] * BW + j;
                                     ++nm;
                                 }
@@ -2138,7 +2153,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                             unsigned f = kNone;
 #pragma unroll
                             for (int j = BW - 1; j >= 0; --j) {
-                                if ((unsigned)j < c && kof(k4[j]) == key) {
+                                if ((unsigned)j < c && k4[j] == key) {
                                     f = h * BW + j;
                                     cb[i] += 1u << 16;
                                 }
@@ -2220,7 +2235,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
                             if (m[i] >= kMulti) continue;
                             const u64 pos = s_base + s_cw[i * NW + wv] + (unsigned)__popcll(bal & lt);
                             if (pos < (u64)a.cap) {
-                                st_s<kNtJoinSt>(orr + pos, WIDE ? (PT)tpay[m[i]] : (PT)(tkey[m[i]] & 0xffffffffull));
+                                st_s<kNtJoinSt>(orr + pos, pay_at(m[i]));
                                 st_s<kNtJoinSt>(oss + pos, (PT)R::pay(sv_[i]));
                             }
                         }
@@ -2493,25 +2508,33 @@ constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
-// i32 rows (k_join_u): threads, build / probe rows per thread, waves per
-// SIMD, workgroups per CU, table slots (log2) and the plan's partition size
-// (log2 of twice the average build rows).  HJ_NARROW_SHAPE picks one for
-// experiment builds (make EXTRA=-DHJ_NARROW_SHAPE=n); the product has one.
+// i32 rows: threads, build / probe rows per thread, waves per SIMD,
+// workgroups per CU, table slots (log2) and the plan's partition size (log2
+// of twice the average build rows); HJ_NARROW_BKT: the bucketed k_join_b (else
+// k_join_u).  HJ_NARROW_SHAPE picks another for experiment builds (make
+// EXTRA=-DHJ_NARROW_SHAPE=n).  REF-B's join (profiles/r03_narrow_shapes.txt):
+// k_join_u over 8192 slots (shape 4, the round-3 start) 1.16 ms; k_join_b
+// 768 x 3+3 0.92 ms (product); 512 x 5+4 at 3 per CU 0.96; 512 x 5+3 at 4
+// per CU 1.35 and 1024 x 3+3 1.12 (both spill at the 64-VGPR cap).
 #ifndef HJ_NARROW_SHAPE
 #define HJ_NARROW_SHAPE 0
 #endif
 #if HJ_NARROW_SHAPE == 1
 constexpr int kNarrowNT = 512, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 8, kNarrowPerCU = 4, kTableLogNarrow = 12,
               kPlanLogNarrow = 12;
-#elif HJ_NARROW_SHAPE == 2
-constexpr int kNarrowNT = 512, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 8, kNarrowPerCU = 4, kTableLogNarrow = 12,
-              kPlanLogNarrow = 11;
-#elif HJ_NARROW_SHAPE == 3
-constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 12,
-              kPlanLogNarrow = 12;
-#else
+#define HJ_NARROW_BKT 0
+#elif HJ_NARROW_SHAPE == 4
 constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
               kPlanLogNarrow = 13;
+#define HJ_NARROW_BKT 0
+#elif HJ_NARROW_SHAPE == 5
+constexpr int kNarrowNT = 512, kNarrowRI = 5, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 3, kTableLogNarrow = 12,
+              kPlanLogNarrow = 12;
+#define HJ_NARROW_BKT 1
+#else
+constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 12,
+              kPlanLogNarrow = 12;
+#define HJ_NARROW_BKT 1
 #endif
 
 int cu_count() {
@@ -2970,20 +2993,28 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                   (k_join_u<true, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
         }
     } else {
-        // i32 rows: k_join_u over an 8192-slot table (the bucketed table's
-        // count + two 16-B reads per probe row lose to one 8-B slot read for
-        // 8-B rows: REF-B 1.42 vs 1.24 ms) unless most build keys repeat;
-        // k_join_grp takes its deferrals (list mode) or, for mostly repeated
-        // keys, every item
+        // i32 rows: k_join_b (keys and row ids apart in LDS: a bucket's 4
+        // keys are one 16-B read) unless most build keys repeat; k_join_grp
+        // takes its deferrals (list mode) or, for mostly repeated keys, every
+        // item
         a.modes = kModeUnique | kModeSome;
         {
             const unsigned gn = items < pgn ? items : pgn;
+#if HJ_NARROW_BKT
+            if (count_only)
+                hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
+                                   dim3(kNarrowNT), 0, st, a);
+            else
+                hipLaunchKernelGGL((k_join_b<false, true, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
+                                   dim3(kNarrowNT), 0, st, a);
+#else
             if (count_only)
                 hipLaunchKernelGGL((k_join_u<false, false, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
                                    dim3(gn), dim3(kNarrowNT), 0, st, a);
             else
                 hipLaunchKernelGGL((k_join_u<false, true, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
                                    dim3(gn), dim3(kNarrowNT), 0, st, a);
+#endif
         }
         a.list = defer_n + 1;
         a.list_n = defer_n;
@@ -3009,7 +3040,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     return hipGetLastError();
 }
 
-hipError_t radix_detect(const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
+hipError_t radix_detect(bool wide, const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
                         unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st) {
     // over the last join's items (work map and descriptors still resident):
     // the items k_join_b built -- the others' kernels answered during the join
@@ -3020,12 +3051,18 @@ hipError_t radix_detect(const RadixPlan &pl, const BucketSet &r, const unsigned 
     a.P = nparts >= 0 ? nparts : 1 << pl.total_bits;
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
-    a.tshift = 64 - pl.skip - pl.total_bits - kTableLog;
+    a.tshift = 64 - pl.skip - pl.total_bits - (wide ? kTableLog : kTableLogNarrow);
     a.dup_flag = dup_flag;
     a.sample = sample;
     a.modes = kModeUnique | kModeSome;
-    hipLaunchKernelGGL((k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS, true>), dim3(2 * cu_count()),
-                       dim3(kFastNT), 0, st, a);
+    if (wide)
+        hipLaunchKernelGGL((k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS, true>), dim3(2 * cu_count()),
+                           dim3(kFastNT), 0, st, a);
+#if HJ_NARROW_BKT
+    else
+        hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS, true>),
+                           dim3(kNarrowPerCU * cu_count()), dim3(kNarrowNT), 0, st, a);
+#endif
     return hipGetLastError();
 }
 
@@ -3046,7 +3083,7 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
         if (stream) return HJ_JOIN_KERNEL_STREAM;
         return m == 2 ? HJ_JOIN_KERNEL_LINEAR : HJ_JOIN_KERNEL_BUCKETED;
     }
-    return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_LINEAR;
+    return m == 2 ? HJ_JOIN_KERNEL_GROUPED : (HJ_NARROW_BKT ? HJ_JOIN_KERNEL_BUCKETED : HJ_JOIN_KERNEL_LINEAR);
 }
 
 }  // namespace hj

@@ -326,7 +326,7 @@ def test_join_kernel_choice_is_deterministic(oracle):
         hk, hp = oracle.gen_uniform_i64(10, 1, 1, 2000, 20000)
         hs, hsp = oracle.gen_uniform_i64(10, 2, 1, 2000, 6000)
         exp_h = oracle.chained_join_i64(hk, hp, hs, hsp, H=200)
-        # i32 unique-ish keys: k_join_u (8192-slot table)
+        # i32 unique-ish keys: k_join_b (keys and row ids apart)
         uk = oracle.gen_uniform_i64(9, 1, 1, 1 << 30, 20000)[0].astype(np.int32)
         us = oracle.gen_uniform_i64(9, 2, 1, 1 << 30, 20000)[0].astype(np.int32)
         us[:4000] = uk[:4000]
@@ -352,7 +352,7 @@ def test_join_kernel_choice_is_deterministic(oracle):
                ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)), ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)),
                ("h", lambda: i64(hk, hp, hs, hsp, exp_h)), ("u32", lambda: i32(uk, us, exp_u)),
                ("h", lambda: i64(hk, hp, hs, hsp, exp_h))]
-        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_b", "u32": "k_join_u", "h": "k_join_u"}
+        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_b", "u32": "k_join_b", "h": "k_join_u"}
         for i, (what, fn) in enumerate(seq):
             assert fn() == want_k[what], f"join {i} ({what})"
     finally:
@@ -429,7 +429,7 @@ def test_radix_bucketed_multi_match(hj, oracle, wide, pattern):
     write all their pairs by a chain walk -- pairs (2 copies), a mix of 2..6
     copies (C1-ref-like), one key 40x, and copies crowding home buckets past
     their 4 slots (chains over several buckets).  int64 rows; the same
-    shapes with i32 rows run k_join_u's per-row walks."""
+    shapes with i32 rows (keys and row ids in separate LDS arrays)."""
     n = 60000
     rng = np.random.default_rng(1234 + len(pattern) + (7 if wide else 0))
     base = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
@@ -457,4 +457,23 @@ def test_radix_bucketed_multi_match(hj, oracle, wide, pattern):
         ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
         assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
     assert hj.has_duplicates()
-    assert hj.join_kernel == ("k_join_b" if wide else "k_join_u")
+    assert hj.join_kernel == "k_join_b"
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_radix_narrow_unprobed_repeats(hj, oracle, dups):
+    """i32 rows through k_join_b: a repeated build key that no probe row meets
+    is still reported (the on-demand DETECT build), and unique keys are not."""
+    n = 120000
+    rng = np.random.default_rng(77)
+    rk = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
+    if dups:
+        rk[5] = rk[77]
+        rk[1000:1030] = rk[999]
+    sk = np.concatenate([rng.choice(rk, size=n // 2), rng.integers(1, 1 << 30, size=n // 2)])
+    sk[np.isin(sk, rk[[5, 999]])] = 3   # (the oracle joins it like any key)
+    o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 6)
+    ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
+    assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
+    assert hj.join_kernel == "k_join_b"
+    assert hj.has_duplicates() == dups
