@@ -747,7 +747,7 @@ __global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, uns
 // exclusive scan (k_scan_*), then place each bucket's runs at its
 // partition's cursor.  Blocks aggregate in LDS first when partitions are
 // few (pass 1: 512).
-constexpr int kListPer = 4;
+constexpr int kListPer = 4;   // (1 or 2 per thread: within 10 %)
 constexpr int kListLds = 4096;
 
 __device__ __forceinline__ unsigned runs_of(unsigned fill) { return (fill + (1u << kRunLog) - 1) >> kRunLog; }
@@ -801,11 +801,26 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
     const u64 base = (u64)blockIdx.x * 1024 * kListPer;
     if (base >= n) return;
-    // bucket j's runs: rows (j << pbl) + 64 k, count min(64, fill - 64 k)
-    auto put_runs = [&](u64 j, unsigned f, u64 at) {
-        for (unsigned k = 0; (k << kRunLog) < f; ++k) {
-            const unsigned cnt = f - (k << kRunLog) < (1u << kRunLog) ? f - (k << kRunLog) : (1u << kRunLog);
-            runs[at + k] = ((((u64)j << pbl) + ((u64)k << kRunLog)) << 7) | cnt;
+    // bucket j's runs: rows (j << pbl) + 64 k, count min(64, fill - 64 k).
+    // Called by the whole wave (every lane, `ok` = it holds a bucket): the
+    // wave writes its buckets' runs cooperatively, R = 2^(pbl - 6) lanes per
+    // bucket, so each store instruction fills 64 / R whole run ranges (one
+    // 128-B line per full 1024-row bucket) instead of 64 scattered 8-B words
+    const unsigned lane_ = threadIdx.x & 63u;
+    auto put_runs = [&](bool ok, u64 j, unsigned f, u64 at) {
+        const int rl = pbl > kRunLog ? (pbl - kRunLog < 6 ? pbl - kRunLog : 6) : 0;
+        const unsigned R = 1u << rl, k0 = lane_ & (R - 1u);
+        for (unsigned b0 = 0; b0 < 64u; b0 += 64u >> rl) {
+            const int src = (int)(b0 + (lane_ >> rl));
+            const bool o = __shfl((int)ok, src) != 0;
+            const unsigned fs = (unsigned)__shfl((int)f, src);
+            const u64 js = ((u64)(unsigned)__shfl((int)(j >> 32), src) << 32) | (unsigned)__shfl((int)j, src);
+            const u64 as = ((u64)(unsigned)__shfl((int)(at >> 32), src) << 32) | (unsigned)__shfl((int)at, src);
+            // (k0 + R m: the rest of a bucket past R runs -- pbl > 12 only)
+            for (unsigned k = k0; o && (k << kRunLog) < fs; k += R) {
+                const unsigned cnt = fs - (k << kRunLog) < (1u << kRunLog) ? fs - (k << kRunLog) : (1u << kRunLog);
+                runs[as + k] = ((((u64)js << pbl) + ((u64)k << kRunLog)) << 7) | cnt;
+            }
         }
     };
     if (P > kListLds) {
@@ -842,10 +857,10 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
             const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)bi[i], (int)l0i[i]);
             const u64 g = ((u64)(unsigned)__builtin_amdgcn_readlane((int)(ri[i] >> 32), (int)l0i[i]) << 32) |
                           (u64)(unsigned)__builtin_amdgcn_readlane((int)ri[i], (int)l0i[i]);
-            if (bi[i] >= (unsigned)P) continue;
+            const bool ok = bi[i] < (unsigned)P;
             const u64 j = base + (u64)i * 1024 + threadIdx.x;
-            const u64 at = pre[i] != ~0u ? rstart[b0] + g + pre[i] : rstart[bi[i]] + ri[i];
-            put_runs(j, fi[i], at);
+            const u64 at = !ok ? 0ull : (pre[i] != ~0u ? rstart[b0] + g + pre[i] : rstart[bi[i]] + ri[i]);
+            put_runs(ok, j, fi[i], at);
         }
         return;
     }
@@ -867,7 +882,8 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
 #pragma unroll
     for (int i = 0; i < kListPer; ++i) {
         const u64 j = base + (u64)i * 1024 + threadIdx.x;
-        if (bn[i] != kNoBucket) put_runs(j, fl[i], cbr[bn[i]] + rr[i]);
+        const bool ok = bn[i] != kNoBucket;
+        put_runs(ok, j, fl[i], ok ? cbr[bn[i]] + rr[i] : 0ull);
     }
 }
 
