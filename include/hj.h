@@ -106,7 +106,9 @@ int64_t hj_ctx_table_capacity(const hj_ctx *ctx);
  * (bits[0..passes-1]); returns 0 passes for GLOBAL / no build. */
 int hj_ctx_radix_plan(const hj_ctx *ctx, int *passes, int bits[3]);
 /* 1 if the build side repeats a key, 0 if not (synchronises).  Known after
- * the build (GLOBAL) or after the first probe (RADIX). */
+ * the build (GLOBAL) or after the first probe (RADIX: a repeat that a probe
+ * row met is flagged by the join; the first call after a join whose kernel
+ * was k_join_b checks the rest of its build partitions on the device). */
 int hj_ctx_build_has_duplicates(hj_ctx *ctx);
 /* Per-phase kernel timing with HIP events on the caller's stream. */
 int hj_ctx_set_timing(hj_ctx *ctx, int enable);
