@@ -263,8 +263,20 @@ def host_leg(hashjoin, seed):
     rc = MR.probe_i64(rk, rp, sk, sp, o_r, o_s)
     t2 = time.perf_counter()
     assert rc == 0 and m == n
+    # the output download alone: M rows x two int64 columns, device -> fresh
+    # host arrays (what the probe must at least spend after the count)
+    import torch
+    d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(2)]
+    h = [np.empty(m, np.int64) for _ in range(2)]
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    for x, y in zip(d, h):
+        torch.from_numpy(y).copy_(x)
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
     return {"api": "hj_count_i64 -> hj_probe_i64 (host memrefs, PCIe Gen5 included)", "rows": "2^24 x 2^24",
             "count_ms": round((t1 - t0) * 1e3, 2), "probe_ms": round((t2 - t1) * 1e3, 2),
+            "download_ms": round((t4 - t3) * 1e3, 2),
             "probe_reused_count_join": hashjoin.lib.hj_host_memo_hits() == h0 + 1,
             "probe_tuples_per_s_end_to_end": round(n / (t2 - t0), 1),
             "pcie_payload_bytes": n * 32 * 2 + m * 16}

@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -788,11 +789,16 @@ struct Joiner {
 //   kHostProbe: if both memrefs digest as the last count's, probe the kept
 //               table with the staged probe side into M-row buffers (no
 //               upload, no build) -- @probeRelation; else the whole join.
+//               The digests run on host threads WHILE the kept table is
+//               probed and, through `deliver`, the pairs are downloaded into
+//               the caller's outputs (speculatively: changed inputs then get
+//               the whole join, whose pairs are delivered again).
 //   kHostJoin:  the whole join (one-memref-out C interface), no memo.
 // Pairs land in dbuf[2], dbuf[3] (not for kHostCount); *m = M.
 enum HostMode { kHostCount, kHostProbe, kHostJoin };
+typedef std::function<int(const void *, const void *, int64_t)> Deliver;
 int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMode mode, int64_t *m, void **d_or,
-              void **d_os) {
+              void **d_os, const Deliver *deliver = nullptr, bool *delivered = nullptr) {
     if (r.n < 0 || s.n < 0) HJ_FAIL(HJ_ERR_ARG, "negative memref size");
     HJ_TRY(set_device(c));
     HJ_TRY(host_stream(c));
@@ -800,17 +806,32 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     const int esz = layout == kWide ? 8 : 4;
     hj_ctx::Memo &mm = c->memo;
     Digest dr, ds;
+    if (delivered) *delivered = false;
     if (mode == kHostProbe && mm.valid && mm.layout == layout && mm.nr == r.n && mm.ns == s.n) {
-        dr = digest_rel(r, esz);
-        ds = digest_rel(s, esz);
-        if (dr == mm.dr && ds == mm.ds) {
-            ++c->memo_hits;
+        int rc = HJ_OK;
+        int64_t mp = 0;
+        bool sent = false;
+        {
+            Joiner dig_r, dig_s;
+            dig_r.t = std::thread([&] { dr = digest_rel(r, esz); });
+            dig_s.t = std::thread([&] { ds = digest_rel(s, esz); });
             const hj::SrcDev src = layout == kWide
                                        ? src_cols64((const int64_t *)c->dbuf[7], (const int64_t *)c->dbuf[7] + s.n, s.n)
                                        : src_col32((const int32_t *)c->dbuf[7], s.n, 0);
-            HJ_TRY(host_probe_all(c, layout, src, (size_t)esz, mm.m, m));
+            rc = host_probe_all(c, layout, src, (size_t)esz, mm.m, &mp);
+            if (rc == HJ_OK && deliver && mp == mm.m) {
+                const int d = (*deliver)(c->dbuf[2], c->dbuf[3], mp);   // (1: outputs of another size, not sent)
+                sent = d == HJ_OK;
+                if (d < 0) rc = d;
+            }
+        }
+        if (rc != HJ_OK) return rc;
+        if (dr == mm.dr && ds == mm.ds) {
+            ++c->memo_hits;
+            *m = mp;
             *d_or = c->dbuf[2];
             *d_os = c->dbuf[3];
+            if (delivered) *delivered = sent;
             return HJ_OK;
         }
     }
@@ -1433,8 +1454,15 @@ int32_t hj_probe_i32(int32_t *, int32_t *r_align, int64_t r_off, int64_t r_size,
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
+    const Deliver put = [&](const void *a, const void *b, int64_t mm) -> int {
+        if (or_size != mm || os_size != mm) return 1;
+        HJ_TRY(download<int32_t>(or_align, or_off, mm, or_stride, a, c->host_stream));
+        return download<int32_t>(os_align, os_off, mm, os_stride, b, c->host_stream);
+    };
+    bool sent = false;
     HJ_TRY(host_join(c, kNarrow, rel32(r_align, r_off, r_size, r_stride), rel32(s_align, s_off, s_size, s_stride),
-                     kHostProbe, &m, &d_or, &d_os));
+                     kHostProbe, &m, &d_or, &d_os, or_size == os_size ? &put : nullptr, &sent));
+    if (sent) return HJ_OK;
     if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
     HJ_TRY(download<int32_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
     HJ_TRY(download<int32_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));
@@ -1468,8 +1496,16 @@ int32_t hj_probe_i64(int64_t *, int64_t *rk, int64_t rk_off, int64_t rk_size, in
     std::lock_guard<std::mutex> host_lk(c->host_mu);
     int64_t m = 0;
     void *d_or = nullptr, *d_os = nullptr;
+    const Deliver put = [&](const void *a, const void *b, int64_t mm) -> int {
+        if (or_size != mm || os_size != mm) return 1;
+        HJ_TRY(download<int64_t>(or_align, or_off, mm, or_stride, a, c->host_stream));
+        return download<int64_t>(os_align, os_off, mm, os_stride, b, c->host_stream);
+    };
+    bool sent = false;
     HJ_TRY(host_join(c, kWide, rel64(rk, rk_off, rk_stride, rp, rp_off, rp_stride, rk_size),
-                     rel64(sk, sk_off, sk_stride, sp, sp_off, sp_stride, sk_size), kHostProbe, &m, &d_or, &d_os));
+                     rel64(sk, sk_off, sk_stride, sp, sp_off, sp_stride, sk_size), kHostProbe, &m, &d_or, &d_os,
+                     or_size == os_size ? &put : nullptr, &sent));
+    if (sent) return HJ_OK;
     if (or_size != m || os_size != m) HJ_FAIL(HJ_ERR_CAPACITY, "output memrefs must have exactly M rows");
     HJ_TRY(download<int64_t>(or_align, or_off, m, or_stride, d_or, c->host_stream));
     HJ_TRY(download<int64_t>(os_align, os_off, m, os_stride, d_os, c->host_stream));

@@ -144,6 +144,16 @@ def test_memref_count_then_probe_reuses_the_join(oracle):
     assert hashjoin.lib.hj_host_memo_hits() == h0 + 3
     assert oracle.same_multiset(o_r, o_s, *exp4)
     assert m4 >= 0
+    # payloads changed, M the same: the probe's speculative delivery of the
+    # kept pairs is overwritten by the fresh join's
+    m5 = MR.count_i64(rk, rp, sk, sp)
+    sp[::5] += 77
+    exp5 = oracle.nested_loop_i64(rk, rp, sk, sp)
+    assert len(exp5[0]) == m5
+    o_r = np.empty(m5, np.int64); o_s = np.empty(m5, np.int64)
+    assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+    assert hashjoin.lib.hj_host_memo_hits() == h0 + 3
+    assert oracle.same_multiset(o_r, o_s, *exp5)
 
 
 def test_memref_concurrent_host_threads(oracle):
