@@ -164,17 +164,22 @@ __global__ __launch_bounds__(256) void k_chunk_count(const u64 *off_a, const u64
     cnt[s] = live ? (len + chunk - 1) / chunk : 0ull;
 }
 
-__global__ __launch_bounds__(256) void k_chunk_finish(const u64 *scan, int nseg, unsigned *start, unsigned *owner) {
-    const int s = blockIdx.x * 256 + threadIdx.x;
+// (2^tl threads per segment: many chunks per segment -- a pass's tiles --
+// fill their owners side by side instead of one thread looping)
+__global__ __launch_bounds__(256) void k_chunk_finish(const u64 *scan, int nseg, unsigned *start, unsigned *owner,
+                                                      int tl) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int s = g >> tl, l = g & ((1 << tl) - 1);
     if (s > nseg) return;
-    start[s] = (unsigned)scan[s];
+    if (l == 0) start[s] = (unsigned)scan[s];
     if (s < nseg)
-        for (u64 w = scan[s]; w < scan[s + 1]; ++w) owner[w] = (unsigned)s;
+        for (u64 w = scan[s] + (u64)l; w < scan[s + 1]; w += (1u << tl)) owner[w] = (unsigned)s;
 }
 
 // --------------------------------------------------------------- scan
-// In-place exclusive scan of a u64 array (3 kernels: block scan, scan of
-// block sums, add).  8192 elements per block.
+// In-place exclusive scan of a u64 array (2 kernels: block scan, then each
+// block adds the sum of the block totals before it, reduced by the block
+// itself).  8192 elements per block.
 constexpr int kScanPer = 8;
 constexpr int kScanBlock = 1024 * kScanPer;
 
@@ -197,21 +202,13 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(u64 *a, u64 n, u64 *sums) 
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_sums(u64 *sums, unsigned nb) {
-    __shared__ u64 wsum[16];
-    u64 carry = 0;
-    for (unsigned b0 = 0; b0 < nb; b0 += 1024) {
-        const unsigned i = b0 + threadIdx.x;
-        const u64 v = i < nb ? sums[i] : 0ull;
-        u64 total;
-        const u64 ex = block_excl_scan<1024>(v, wsum, &total);
-        if (i < nb) sums[i] = carry + ex;
-        carry += total;
-    }
-}
-
 __global__ __launch_bounds__(1024) void k_scan_add(u64 *a, u64 n, const u64 *sums) {
-    const u64 add = sums[blockIdx.x];
+    __shared__ u64 wsum[16];
+    if (blockIdx.x == 0) return;   // (uniform: block 0 adds nothing)
+    u64 v = 0;
+    for (unsigned i = threadIdx.x; i < blockIdx.x; i += 1024) v += sums[i];
+    u64 add;
+    block_excl_scan<1024>(v, wsum, &add);
     const u64 base = (u64)blockIdx.x * kScanBlock;
     for (int i = threadIdx.x; i < kScanBlock; i += 1024)
         if (base + i < n) a[base + i] += add;
@@ -2577,18 +2574,20 @@ unsigned pass_grid(u64 n) {
 void scan_u64(u64 *v, u64 len, u64 *sums, hipStream_t st) {
     const unsigned nb = blocks_for(len, kScanBlock);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, v, len, sums);
-    if (nb > 1) {
-        hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, st, sums, nb);
-        hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, v, len, (const u64 *)sums);
-    }
+    if (nb > 1) hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, v, len, (const u64 *)sums);
 }
 
+// per_seg: about how many chunks a segment has (sizes the owner fill's
+// threads per segment)
 void chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, unsigned *start, unsigned *owner,
-               u64 *scratch, u64 *sums, hipStream_t st) {
+               u64 *scratch, u64 *sums, hipStream_t st, u64 per_seg = 1) {
     const unsigned g = blocks_for((u64)nseg + 1, 256);
     hipLaunchKernelGGL(k_chunk_count, dim3(g), dim3(256), 0, st, off_a, off_b, nseg, chunk, scratch);
     scan_u64(scratch, (u64)nseg + 1, sums, st);
-    hipLaunchKernelGGL(k_chunk_finish, dim3(g), dim3(256), 0, st, (const u64 *)scratch, nseg, start, owner);
+    int tl = 0;
+    while (tl < 6 && (2ull << tl) <= per_seg) ++tl;
+    hipLaunchKernelGGL(k_chunk_finish, dim3(blocks_for(((u64)nseg + 1) << tl, 256)), dim3(256), 0, st,
+                       (const u64 *)scratch, nseg, start, owner, tl);
 }
 
 }  // namespace
@@ -2810,7 +2809,7 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
             // tiles of kTile / 64 runs per segment, tile -> segment, and one
             // descriptor per tile
             chunk_map(prev->rstart, nullptr, nseg, (unsigned)(kTile >> kRunLog), ws.tile_start, ws.tile_owner, ws.pcur,
-                      ws.scan_sums, st);
+                      ws.scan_sums, st, (u64)n / (u64)(nseg > 0 ? nseg : 1) / (u64)kTile);
             const u64 tb = radix_tiles((long long)n, nseg);
             hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, st, (const unsigned *)ws.tile_start,
                                (const unsigned *)ws.tile_owner, (const u64 *)prev->rstart, nseg, (unsigned)tb,
