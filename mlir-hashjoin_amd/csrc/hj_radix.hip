@@ -906,6 +906,10 @@ struct JoinArgs {
     // repeated}; modes: bit m = this launch runs when sample_mode() == m
     const u64 *sample = nullptr;
     unsigned modes = 7u;
+    // k_join_b (i32 rows): items past a workgroup's first two are handed out
+    // by this counter (zeroed by k_item_desc) instead of w += grid, so
+    // workgroups that drew heavy items (a hot key's chunks) take fewer
+    unsigned *next_item = nullptr;
 };
 
 constexpr unsigned kModeUnique = 1u, kModeSome = 2u, kModeMostlyRepeated = 4u;
@@ -983,10 +987,11 @@ struct ItemDesc {
 // (scalar) load instead of the owner -> partition -> offsets chain.
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
                                                    const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
-                                                   ItemDesc *desc, unsigned *zero, unsigned *zero2) {
+                                                   ItemDesc *desc, unsigned *zero, unsigned *zero2, unsigned *zero3) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
     if (w == 0 && zero) *zero = 0u;
     if (w == 0 && zero2) *zero2 = 0u;
+    if (w == 0 && zero3) *zero3 = 0u;
     if (w >= work_start[P]) return;
     const int p = (int)work_owner[w];
     const unsigned c = w - work_start[p];
@@ -1881,6 +1886,14 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     __shared__ unsigned s_cw[SI * NW + NW];
     __shared__ unsigned s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
     __shared__ unsigned s_mpre[NT];   // a thread's multi pairs before it in its wave (kept out of registers)
+    // a.next_item (i32 rows; int64 rows and DETECT walk w += grid: the wide
+    // instantiation has no SGPRs left for it, its next item's run entries
+    // already fill them -- with the claim it spilled 20 B and lost 6 % on C3
+    // while C4 gained 5 %, profiles/r03_narrow_shapes.txt 6): iteration k claims the
+    // item of iteration k + 2 into s_next after its first barrier, and the top
+    // of iteration k + 1 reads it (a workgroup's first two items are static:
+    // blockIdx.x, blockIdx.x + grid)
+    __shared__ unsigned s_next;
     bool dup_sent = false;
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
@@ -1949,6 +1962,11 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     ents(a.r_runs, it.r_lo, it.r_hi, er, RI);
     // (DETECT reads no probe rows)
     if (!DETECT) ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    constexpr bool dyn = !DETECT && !WIDE;
+    if (dyn) {
+        if (threadIdx.x == 0) s_next = w + gridDim.x;
+        __syncthreads();
+    }
     while (true) {
         const bool fits = it.r_hi - it.r_lo <= (u64)rmax;
         unsigned rok = 0, sok = 0;
@@ -1956,16 +1974,22 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             rok = rows_of(rrows, er, rv_, RI);
             if (!DETECT) sok = rows_of(srows, es, sv_, SI);
         }
-        const bool more = w + gridDim.x < total;
+        const unsigned wn = dyn ? __builtin_amdgcn_readfirstlane(s_next) : w + gridDim.x;
+        const bool more = wn < total;
         u64 ner[RI], nes[SI];
         ItemDesc nx = it;
         if (more) {
-            nx = sload(a.desc + w + gridDim.x);
+            nx = sload(a.desc + wn);
             ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
             if (!DETECT) ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
         }
         if (!fits) {
             if (!DETECT && threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            if (dyn) {   // (every thread has read s_next above; the claim is read next iteration)
+                __syncthreads();
+                if (threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
+                __syncthreads();
+            }
         } else {
             // (zeros from the item's descriptor -- r_lo < 2^63 -- or the
             // compiler keeps a constant zero quad live across the loop and
@@ -1982,6 +2006,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             else if (DETECT && ci < NB / 2) ((uint4 *)bsig)[ci - NB / 4] = z4;
             if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
             __syncthreads();
+            if (dyn && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
             // ---- build: every row's rank add issued before any is used
             bool bad = false;
             for (u64 r0 = it.r_lo;;) {
@@ -2265,7 +2290,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             __syncthreads();   // table reused by the next item
         }
         if (!more) break;
-        w += gridDim.x;
+        w = wn;
         it = nx;
 #pragma unroll
         for (int i = 0; i < RI; ++i) er[i] = ner[i];
@@ -2648,7 +2673,7 @@ unsigned long long radix_tiles(long long n, int max_nseg) {
 size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
 
 unsigned long long radix_work_words(const RadixPlan &pl, unsigned long long s_runs) {
-    return (1ull << pl.total_bits) + 3ull + 3ull * radix_join_items(pl, s_runs);
+    return (1ull << pl.total_bits) + 4ull + 3ull * radix_join_items(pl, s_runs);
 }
 
 hipError_t exclusive_scan_u64(unsigned long long *v, unsigned long long len, unsigned long long *sums,
@@ -2962,9 +2987,10 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     // (for k_join, or for k_join_grp with i32 rows), then k_join_grp's
     unsigned *defer_n = work_owner + radix_join_items(pl, s_runs);
     unsigned *defer2_n = defer_n + 1 + radix_join_items(pl, s_runs);
+    unsigned *next_item = defer2_n + 1 + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n);
+                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n, next_item);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -3016,12 +3042,14 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         {
             const unsigned gn = items < pgn ? items : pgn;
 #if HJ_NARROW_BKT
+            a.next_item = next_item;
             if (count_only)
                 hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
                                    dim3(kNarrowNT), 0, st, a);
             else
                 hipLaunchKernelGGL((k_join_b<false, true, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
                                    dim3(kNarrowNT), 0, st, a);
+            a.next_item = nullptr;
 #else
             if (count_only)
                 hipLaunchKernelGGL((k_join_u<false, false, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
