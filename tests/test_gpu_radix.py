@@ -477,3 +477,33 @@ def test_radix_narrow_unprobed_repeats(hj, oracle, dups):
     assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
     assert hj.join_kernel == "k_join_b"
     assert hj.has_duplicates() == dups
+
+
+@pytest.mark.parametrize("wide", [True, False])
+def test_radix_detect_many_suspects(hj, oracle, wide):
+    """The on-demand repeat check when one partition holds more suspects than
+    k_join_b's suspect list (512): every live slot of that table checks its
+    chain instead.  Partition 0 of a 6-bit plan gets 40 keys x 25 copies on
+    top of its share of unique keys (~2560 rows, under the 3/4-table defer
+    limit); no probe row meets a repeated key, so only the check can report
+    them."""
+    rng = np.random.default_rng(4242)
+    cand = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=400000, replace=False)
+    top6 = ((cand.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(58)).astype(np.int64)
+    hot = cand[top6 == 0][:40]
+    rest = cand[top6 != 0]
+    uniq = np.concatenate([cand[top6 == 0][40:40 + 1560], rest[:98440]])
+    rk = np.concatenate([uniq, np.repeat(hot, 25)])
+    rng.shuffle(rk)
+    sk = np.concatenate([rng.choice(uniq, size=60000), rng.integers(1 << 30, 1 << 31, size=20000)])
+    rp = np.arange(len(rk), dtype=np.int64) * 7 + 3
+    sp = np.arange(len(sk), dtype=np.int64) * 11 + 5
+    if wide:
+        o = run(hj, rk, rp, sk, sp, 6)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
+    else:
+        o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 6)
+        ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
+        assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
+    assert hj.join_kernel == "k_join_b"
+    assert hj.has_duplicates()
