@@ -1852,12 +1852,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 // i32 rows keep keys and row ids apart (a bucket's keys are one 16-B read);
 // an item whose probe rows would write many pairs per row (the reference's
 // keys in [1, 100k]) goes to k_join_grp before anything of it is written.
-template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false>
+template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false, int TSL = 12>
 __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     typedef typename std::conditional<WIDE, u64, unsigned>::type PT;
-    constexpr int TS = 4096;
+    constexpr int TS = 1 << TSL;   // table slots (a.tshift is set for TSL hash bits)
     constexpr int BW = 4;
     constexpr int NB = TS / BW;
     constexpr unsigned kBMask = NB - 1;
@@ -1998,12 +1998,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             const uint4 z4 = make_uint4(z, z, z, z);
             // (thread 0 clears the control words: it is also the one that
             // reads the previous item's s_dup after the item's last barrier)
-            static_assert(NB / 2 <= NT, "one 16-B clear per thread: counts, signatures");
+            static_assert(NB / 4 <= NT, "one 16-B clear per thread: bucket words");
             // (the index carries z too: a loop-invariant clear address was
             // hoisted out of the item loop and spilled)
             const unsigned ci = threadIdx.x + z;
             if (ci < NB / 4) ((uint4 *)bcnt)[ci] = z4;
-            else if (DETECT && ci < NB / 2) ((uint4 *)bsig)[ci - NB / 4] = z4;
+            if (DETECT)
+                for (unsigned j = ci; j < NB / 4; j += NT) ((uint4 *)bsig)[j] = z4;
             if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
             __syncthreads();
             if (dyn && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
@@ -2292,10 +2293,11 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
         if (!more) break;
         w = wn;
         it = nx;
-#pragma unroll
+        // (plain loops: with DETECT's unused S entries the unroll pragma
+        // could not be honoured for its instantiation and warned)
         for (int i = 0; i < RI; ++i) er[i] = ner[i];
-#pragma unroll
-        for (int i = 0; i < SI; ++i) es[i] = nes[i];
+        if constexpr (!DETECT)
+            for (int i = 0; i < SI; ++i) es[i] = nes[i];
     }
 }
 
@@ -2552,8 +2554,11 @@ constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 
 // k_join_u).  HJ_NARROW_SHAPE picks another for experiment builds (make
 // EXTRA=-DHJ_NARROW_SHAPE=n).  REF-B's join (profiles/r03_narrow_shapes.txt):
 // k_join_u over 8192 slots (shape 4, the round-3 start) 1.16 ms; k_join_b
-// 768 x 3+3 0.92 ms (product); 512 x 5+4 at 3 per CU 0.96; 512 x 5+3 at 4
-// per CU 1.35 and 1024 x 3+3 1.12 (both spill at the 64-VGPR cap).
+// over 4096 slots: 768 x 3+3 0.92 ms (shape 7), 512 x 5+4 at 3 per CU 0.96,
+// 512 x 5+3 at 4 per CU 1.35 and 1024 x 3+3 1.12 (both spill at the 64-VGPR
+// cap); k_join_b over 8192 slots (keys + row ids 64 KiB, partitions of ~3000
+// rows: half the items): 768 x 3+3 0.886 (shape 6), 768 x 4+4 0.779
+// (product); 4+6 and 5+5 spill.
 #ifndef HJ_NARROW_SHAPE
 #define HJ_NARROW_SHAPE 0
 #endif
@@ -2569,9 +2574,18 @@ constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNa
 constexpr int kNarrowNT = 512, kNarrowRI = 5, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 3, kTableLogNarrow = 12,
               kPlanLogNarrow = 12;
 #define HJ_NARROW_BKT 1
-#else
+#elif HJ_NARROW_SHAPE == 6
+constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
+              kPlanLogNarrow = 13;
+#define HJ_NARROW_BKT 1
+#elif HJ_NARROW_SHAPE == 7
 constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 12,
               kPlanLogNarrow = 12;
+#define HJ_NARROW_BKT 1
+
+#else
+constexpr int kNarrowNT = 768, kNarrowRI = 4, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
+              kPlanLogNarrow = 13;
 #define HJ_NARROW_BKT 1
 #endif
 
@@ -3044,11 +3058,13 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
 #if HJ_NARROW_BKT
             a.next_item = next_item;
             if (count_only)
-                hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
-                                   dim3(kNarrowNT), 0, st, a);
+                hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS, false,
+                                             kTableLogNarrow>),
+                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
             else
-                hipLaunchKernelGGL((k_join_b<false, true, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>), dim3(gn),
-                                   dim3(kNarrowNT), 0, st, a);
+                hipLaunchKernelGGL((k_join_b<false, true, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS, false,
+                                             kTableLogNarrow>),
+                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
             a.next_item = nullptr;
 #else
             if (count_only)
@@ -3103,7 +3119,10 @@ hipError_t radix_detect(bool wide, const RadixPlan &pl, const BucketSet &r, cons
                            dim3(kFastNT), 0, st, a);
 #if HJ_NARROW_BKT
     else
-        hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS, true>),
+        // (its signature words and suspect list on top of the table: one
+        // workgroup per CU at 8192 slots: 3 waves per SIMD, register budget as for 4)
+        hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, (kTableLogNarrow > 12 ? 3 : kNarrowWPS),
+                                     true, kTableLogNarrow>),
                            dim3(kNarrowPerCU * cu_count()), dim3(kNarrowNT), 0, st, a);
 #endif
     return hipGetLastError();
