@@ -2543,8 +2543,11 @@ constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
 // probe sides much larger than the build side (C2: 2^30 x 2^20, ~1000 S rows
 // per R row): many sub-chunks per item, so bigger sub-chunks and more waves
 // (1024 threads x 4 S rows, 8 waves per SIMD): C2 join 9.45 -> 8.77 ms, C3
-// 2.79 -> 3.32 ms (profiles/r02_join_shapes.txt)
-constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 4, kStreamWPS = 8;
+// 2.79 -> 3.32 ms (profiles/r02_join_shapes.txt).  3 S rows per thread since
+// round 3: the 4-row shape carried a 12-B scratch spill at the 64-VGPR cap;
+// without it C2's join 6.49 -> 6.16 ms on one box (768 x 3+4: 6.25, 768 x
+// 2+5: 6.30, 1024 x 1+4: 6.47; profiles/r03_narrow_shapes.txt 8)
+constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 3, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
