@@ -130,11 +130,6 @@ struct hj_ctx {
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
     Buf route_hist, route_sums;               // folded routing: (bin, workgroup) slot bases, scan sums
-    unsigned long long *h_rstart = nullptr;   // chunked probe: S's first-pass segment starts (pinned)
-    size_t h_rstart_n = 0;
-    hipStream_t join_stream2 = nullptr;       // chunked probe: the joins' stream
-    hipEvent_t chunk_ev[2] = {nullptr, nullptr};
-    Buf pcur2, sums2;                         // ... and their chunk-map scratch
     // timing
     bool timing = false;
     bool ev_ready = false;
@@ -402,128 +397,6 @@ bool use_xcd_split(const hj_ctx *c, int layout, int64_t n) {
     return n >= kXcdMinRows && table > kXcdMinTable && table <= kXcdMaxTable;
 }
 
-// HJ_CHUNKS=K (experiment): S's second pass and the join run chunk by chunk
-// over K groups of first-pass segments, so each chunk's pass-2 output is read
-// back by its join while it is still in the Infinity Cache.
-int probe_chunks() {
-    static const int k = [] {
-        const char *e = getenv("HJ_CHUNKS");
-        return e ? atoi(e) : 0;
-    }();
-    return k;
-}
-
-int do_probe_chunked(hj_ctx *c, const hj::SrcDev &src, void *out_r, void *out_s, int64_t cap, uint64_t *d_count,
-                     bool count_only, hipStream_t st, int K) {
-    const hj::RadixPlan &pl = c->plan;
-    const size_t esz = 16;
-    const int F1 = 1 << pl.bits[0], F2 = 1 << pl.bits[1];
-    const size_t P = size_t(1) << pl.total_bits;
-    HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, esz, pl));
-    if (c->h_rstart_n < (size_t)F1 + 1) {
-        if (c->h_rstart) HJ_HIP(hipHostFree(c->h_rstart));
-        c->h_rstart = nullptr;
-        HJ_HIP(hipHostMalloc((void **)&c->h_rstart, (F1 + 1) * 8));
-        c->h_rstart_n = (size_t)F1 + 1;
-    }
-    record(c, kEvProbe0, st);
-    hj::RadixPlan p1 = pl;
-    p1.passes = 1;
-    const hj::BucketSet tmp = bucket_set(c->tset);
-    HJ_HIP(hj::radix_partition(src, true, p1, radix_work(c), tmp, st));
-    record(c, kEvProbeMid, st);
-    HJ_HIP(hipMemcpyAsync(c->h_rstart, tmp.rstart, (F1 + 1) * 8, hipMemcpyDeviceToHost, st));
-    HJ_HIP(hipStreamSynchronize(st));
-    const unsigned long long *rs = c->h_rstart;
-    const unsigned long long total = rs[F1];
-    // chunk boundaries: about total / K runs each
-    std::vector<int> seg0{0};
-    for (int k = 1; k < K; ++k) {
-        const unsigned long long want = total * (unsigned long long)k / (unsigned long long)K;
-        int s = seg0.back() + 1;
-        while (s < F1 && rs[s] < want) ++s;
-        if (s < F1 && s > seg0.back()) seg0.push_back(s);
-    }
-    seg0.push_back(F1);
-    const int nch = (int)seg0.size() - 1;
-    std::vector<hj::RadixNeed> need(nch);
-    unsigned long long nbk = 0;
-    for (int i = 0; i < nch; ++i) {
-        const unsigned long long runs = rs[seg0[i + 1]] - rs[seg0[i]];
-        need[i] = hj::radix_need_from((long long)(runs << hj::kRunLog), runs, seg0[i + 1] - seg0[i], pl, 1);
-        nbk += need[i].buckets;
-    }
-    HJ_TRY(ensure_set(c->sset, hj::RadixNeed{nbk, nbk << pl.pbl[1]}, esz, P + (size_t)nch));
-    HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, esz, pl));
-    const hj::BucketSet sfull = bucket_set(c->sset), rfull = bucket_set(c->rset);
-    // HJ_CHUNK_STREAMS=2: the joins on a second stream, each waiting for its
-    // chunk's pass (pass i + 1 overlaps join i)
-    static const bool two = [] {
-        const char *e = getenv("HJ_CHUNK_STREAMS");
-        return e && atoi(e) == 2;
-    }();
-    hipStream_t jst = st;
-    hj::RadixWork jws = radix_work(c);
-    if (two) {
-        if (!c->join_stream2) HJ_HIP(hipStreamCreateWithFlags(&c->join_stream2, hipStreamNonBlocking));
-        for (hipEvent_t &e : c->chunk_ev)
-            if (!e) HJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HJ_TRY(ensure_buf(c->pcur2, (P + 1) * 8));
-        HJ_TRY(ensure_buf(c->sums2, ((P + 1) / 8192 + 2) * 8));
-        jws.pcur = (unsigned long long *)c->pcur2.p;
-        jws.scan_sums = (unsigned long long *)c->sums2.p;
-        jst = c->join_stream2;
-    }
-    unsigned long long b0 = 0, u0 = 0;
-    // HJ_CHUNK_SPLIT=1 (control): every chunk's pass first, then the joins --
-    // the same launches and tails without the cache hand-off
-    static const bool split = getenv("HJ_CHUNK_SPLIT") != nullptr;
-    std::vector<hj::BucketSet> svs(nch);
-    for (int pass_i = 0; pass_i < (split ? 2 * nch : nch); ++pass_i) {
-        const int i = split ? (pass_i < nch ? pass_i : pass_i - nch) : pass_i;
-        const bool do_pass = !split || pass_i < nch, do_join = !split || pass_i >= nch;
-        const int a = seg0[i], nseg = seg0[i + 1] - a;
-        const unsigned long long runs = rs[seg0[i + 1]] - rs[a];
-        hj::BucketSet prev = tmp;
-        prev.rstart = tmp.rstart + a;
-        hj::BucketSet &sv = svs[i];
-        if (do_pass) {
-            sv = sfull;
-            sv.rows = (char *)sfull.rows + (b0 << pl.pbl[1]) * esz;
-            sv.bbin = sfull.bbin + b0;
-            sv.bfill = sfull.bfill + b0;
-            sv.max_buckets = (unsigned)need[i].buckets;
-            sv.max_rows = need[i].rows;
-            sv.max_runs = (need[i].rows >> hj::kRunLog) + need[i].buckets;
-            sv.runs = sfull.runs + u0;
-            sv.rstart = sfull.rstart + (size_t)a * F2 + i;
-            b0 += need[i].buckets;
-            u0 += sv.max_runs;
-            HJ_HIP(hj::radix_partition_from(true, pl, 1, prev, nseg, (long long)(runs << hj::kRunLog), radix_work(c),
-                                            sv, st));
-        }
-        if (!do_join) continue;
-        hj::BucketSet rv = rfull;
-        rv.rstart = rfull.rstart + (size_t)a * F2;
-        if (two) {
-            HJ_HIP(hipEventRecord(c->chunk_ev[0], st));
-            HJ_HIP(hipStreamWaitEvent(jst, c->chunk_ev[0], 0));
-        }
-        HJ_HIP(hj::radix_join(true, pl, jws, rv, sv, sv.max_runs, (unsigned *)c->work_start.p, c->work_desc.p, out_r,
-                              out_s, count_only ? 0 : cap, (unsigned long long *)d_count, c->meta + 1, count_only, jst,
-                              c->meta + 2, false, nseg * F2));
-    }
-    if (two) {
-        HJ_HIP(hipEventRecord(c->chunk_ev[1], jst));
-        HJ_HIP(hipStreamWaitEvent(st, c->chunk_ev[1], 0));
-    }
-    c->join_ran = false;   // (no single work map to re-check repeats over)
-    record(c, kEvProbe1, st);
-    c->rec[2] = c->timing;
-    c->rec_mid = c->timing;
-    return HJ_OK;
-}
-
 int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *out_s, int64_t cap,
              uint64_t *d_count, bool count_only, hipStream_t st) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
@@ -536,9 +409,6 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     const bool radix = c->used == HJ_STRATEGY_RADIX || (c->dual && src.n >= kRadixProbeMinRows);
     c->probe_used = radix ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
     c->join_ran = false;
-    if (radix && layout == kWide && c->plan.passes == 2 && c->plan.skip == 0 && probe_chunks() > 1 &&
-        src.n < 8 * c->n_build)
-        return do_probe_chunked(c, src, out_r, out_s, cap, d_count, count_only, st, probe_chunks());
     if (radix) {
         const bool wide = layout == kWide;
         const size_t esz = wide ? 16 : 8;
@@ -1174,12 +1044,6 @@ void hj_ctx_destroy(hj_ctx *c) {
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
                    &c->route_hist, &c->route_sums})
         free_buf(*b);
-    if (c->h_rstart) (void)hipHostFree(c->h_rstart);
-    if (c->join_stream2) (void)hipStreamDestroy(c->join_stream2);
-    for (hipEvent_t &e : c->chunk_ev)
-        if (e) (void)hipEventDestroy(e);
-    free_buf(c->pcur2);
-    free_buf(c->sums2);
     if (c->ev_ready)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
     {

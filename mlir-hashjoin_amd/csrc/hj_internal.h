@@ -200,14 +200,6 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,
                       const unsigned long long *sample, bool stream, int nparts = -1);
-// Chunked probe: passes first .. end of plan pl over nseg segments of a
-// bucketed input `prev` (a view whose rstart starts at the chunk's first
-// segment; runs and rows stay absolute) into `out`; n_bound >= their rows.
-hipError_t radix_partition_from(bool wide, const RadixPlan &pl, int first, const BucketSet &prev, int nseg,
-                                long long n_bound, const RadixWork &ws, const BucketSet &out, hipStream_t st);
-// Bucket capacity of pass `pass` of plan pl over nseg input segments holding
-// `runs` runs (<= n rows).
-RadixNeed radix_need_from(long long n, unsigned long long runs, int nseg, const RadixPlan &pl, int pass);
 // Folded routing's send side: rows (int64 columns or packed tuples) grouped
 // by the top rbits (<= 9) of radix_hash into out_tuples, exact and contiguous
 // per bin, bins in order; counts[2^rbits] their sizes.  One EXACT partition

@@ -2976,27 +2976,6 @@ hipError_t radix_partition_routed(const void *tuples, long long n, const unsigne
     return radix_passes(src, (u64)(n > 0 ? n : 0), true, pl, 1, &in, nseg, ws, out, st);
 }
 
-RadixNeed radix_need_from(long long n, unsigned long long runs, int nseg, const RadixPlan &pl, int pass) {
-    // as radix_need, for one pass over a bucketed input of `runs` runs in nseg
-    // segments (tiles of kTile / 64 runs, <= one partial tile per segment)
-    const u64 rows = n > 0 ? (u64)n : 1;
-    const u64 G = pass_grid(rows);
-    const u64 F = 1ull << pl.bits[pass];
-    const u64 tiles = (u64)runs / (kTile >> kRunLog) + (u64)nseg + 1;
-    const u64 b = (tiles * kTile >> pl.pbl[pass]) + G + ((u64)nseg + G) * F + G + 1;
-    return RadixNeed{b, b << pl.pbl[pass]};
-}
-
-hipError_t radix_partition_from(bool wide, const RadixPlan &pl, int first, const BucketSet &prev, int nseg,
-                                long long n_bound, const RadixWork &ws, const BucketSet &out, hipStream_t st) {
-    if (first < 1 || first >= pl.passes || nseg < 1) return hipErrorInvalidValue;
-    SrcDev src{};
-    src.key = prev.rows;
-    src.n = n_bound;
-    src.form = kPacked64;
-    return radix_passes(src, (u64)(n_bound > 0 ? n_bound : 0), wide, pl, first, &prev, nseg, ws, out, st);
-}
-
 hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, const BucketSet &s,
                       unsigned long long s_runs, unsigned *work_start, void *desc, void *out_r, void *out_s, long long cap,
                       unsigned long long *counter, unsigned long long *dup_flag, bool count_only, hipStream_t st,

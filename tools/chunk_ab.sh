@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Runs against the library of commit b41946e: the HJ_CHUNKS code was removed after the measurement, profiles/r03_chunked_handoff.txt.)
 # A/B of the chunked probe (HJ_CHUNKS, HJ_CHUNK_STREAMS): C3 bench lines with verification, then a kernel trace.
 set -e
 mkdir -p gpurun_out/chunk

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Runs against the library of commit b41946e: the HJ_CHUNKS code was removed after the measurement, profiles/r03_chunked_handoff.txt.)
 # Does S's pass-2 -> join hand-off come from the Infinity Cache?  Chunked probe (HJ_CHUNKS=K) with each
 # chunk's join right after its pass ("inter") against every pass first, then every join ("split": the
 # same launches and tails, no hand-off).  Kernel traces of each; summarised by tools/chunk_summary.py.
