@@ -51,6 +51,11 @@ constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build 
 constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
 constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
+// Join items of multi-chunk partitions first (k_item_desc); 0 = partition order.
+#ifndef HJ_HEAVY_FIRST
+#define HJ_HEAVY_FIRST 1
+#endif
+constexpr bool kHeavyFirst = HJ_HEAVY_FIRST != 0;
 constexpr int kPassPbl = 10;       // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return radix_hash(k); }
@@ -151,8 +156,10 @@ __device__ __forceinline__ u64 block_excl_scan(u64 v, u64 *wsum, u64 *total) {
 // off_b is given and segment s of b is empty (no build rows -> nothing to
 // join); start = exclusive scan of count (scan_u64), and owner[w] = the
 // segment of chunk w, so consumers need one load instead of a search.
+// split: the high half of each count word also counts the chunks of
+// segments with >= 2 of them (their scan: k_item_desc's heavy-first order).
 __global__ __launch_bounds__(256) void k_chunk_count(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk,
-                                                     u64 *cnt) {
+                                                     u64 *cnt, bool split) {
     const int s = blockIdx.x * 256 + threadIdx.x;
     if (s > nseg) return;
     if (s == nseg) {
@@ -161,7 +168,8 @@ __global__ __launch_bounds__(256) void k_chunk_count(const u64 *off_a, const u64
     }
     const u64 len = off_a[s + 1] - off_a[s];
     const bool live = off_b ? (off_b[s + 1] > off_b[s]) : true;
-    cnt[s] = live ? (len + chunk - 1) / chunk : 0ull;
+    const u64 c = live ? (len + chunk - 1) / chunk : 0ull;
+    cnt[s] = split && c >= 2 ? c | (c << 32) : c;
 }
 
 // (2^tl threads per segment: many chunks per segment -- a pass's tiles --
@@ -173,7 +181,7 @@ __global__ __launch_bounds__(256) void k_chunk_finish(const u64 *scan, int nseg,
     if (s > nseg) return;
     if (l == 0) start[s] = (unsigned)scan[s];
     if (s < nseg)
-        for (u64 w = scan[s] + (u64)l; w < scan[s + 1]; w += (1u << tl)) owner[w] = (unsigned)s;
+        for (u64 w = (unsigned)scan[s] + (u64)l; w < (unsigned)scan[s + 1]; w += (1u << tl)) owner[w] = (unsigned)s;
 }
 
 // --------------------------------------------------------------- scan
@@ -985,9 +993,16 @@ struct ItemDesc {
 
 // One descriptor per work item, so the join reads its item with one
 // (scalar) load instead of the owner -> partition -> offsets chain.
+// Items of partitions with >= 2 chunks (a skewed key's: heavy) come first,
+// then the one-chunk items, each group in partition order (split scan of
+// k_chunk_count: heavy chunks before partition p in the high half).  The
+// join kernels stride items w = wg, wg + grid, ...: heavy items then spread
+// evenly over the workgroups instead of landing where their partitions fall
+// (C4 Zipf: join 2.89 -> 2.71 ms, profiles/r03_heavy_first.txt; int64 rows only).
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
                                                    const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
-                                                   ItemDesc *desc, unsigned *zero, unsigned *zero2, unsigned *zero3) {
+                                                   ItemDesc *desc, unsigned *zero, unsigned *zero2, unsigned *zero3,
+                                                   const u64 *split) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
     if (w == 0 && zero) *zero = 0u;
     if (w == 0 && zero2) *zero2 = 0u;
@@ -1001,7 +1016,13 @@ __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, c
     d.s_hi = d.s_lo + chr < e ? d.s_lo + chr : e;
     d.r_lo = r_rstart[p];
     d.r_hi = r_rstart[p + 1];
-    desc[w] = d;
+    unsigned at = w;
+    if (split) {
+        const unsigned hp = (unsigned)(split[p] >> 32);
+        at = work_start[p + 1] - work_start[p] >= 2 ? hp + c
+                                                    : (unsigned)(split[P] >> 32) + (work_start[p] - hp);
+    }
+    desc[at] = d;
 }
 
 // A persistent workgroup of NT threads walks work items w = wg, wg + grid, ...
@@ -2622,9 +2643,9 @@ void scan_u64(u64 *v, u64 len, u64 *sums, hipStream_t st) {
 // per_seg: about how many chunks a segment has (sizes the owner fill's
 // threads per segment)
 void chunk_map(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, unsigned *start, unsigned *owner,
-               u64 *scratch, u64 *sums, hipStream_t st, u64 per_seg = 1) {
+               u64 *scratch, u64 *sums, hipStream_t st, u64 per_seg = 1, bool split = false) {
     const unsigned g = blocks_for((u64)nseg + 1, 256);
-    hipLaunchKernelGGL(k_chunk_count, dim3(g), dim3(256), 0, st, off_a, off_b, nseg, chunk, scratch);
+    hipLaunchKernelGGL(k_chunk_count, dim3(g), dim3(256), 0, st, off_a, off_b, nseg, chunk, scratch, split);
     scan_u64(scratch, (u64)nseg + 1, sums, st);
     int tl = 0;
     while (tl < 6 && (2ull << tl) <= per_seg) ++tl;
@@ -2998,7 +3019,11 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     u64 chb = (u64)kJoinSub * subb;
     const u64 want = (u64)s_runs / (16ull * (wide ? pg : pgn));
     if (want > chb) chb = (want + subb - 1) / subb * subb;
-    chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    // heavy-first item order: int64 rows (static item striding); i32 rows
+    // claim items dynamically and k_join_grp lost 0.2 ms on REF-A with it
+    const bool heavy_first = kHeavyFirst && wide;
+    chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st, 1,
+              heavy_first);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
     // the deferred-item lists live after the work map: the fast kernels'
     // (for k_join, or for k_join_grp with i32 rows), then k_join_grp's
@@ -3007,7 +3032,8 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     unsigned *next_item = defer2_n + 1 + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n, next_item);
+                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n, next_item,
+                       heavy_first ? (const u64 *)ws.pcur : nullptr);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;

@@ -238,6 +238,25 @@ def test_radix_hot_key_tiles(hj, oracle, bits):
     assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=4096))
 
 
+@pytest.mark.parametrize("bits", [12, 17])
+def test_radix_heavy_items_first(hj, oracle, bits):
+    """Half of 2^21 S rows on 40 hot keys of Zipf-like weights: their
+    partitions split into several work items each (the rest one item), and
+    the join lists those items first (k_item_desc's heavy-first order) --
+    every pair still comes out exactly once."""
+    rng = np.random.default_rng(23)
+    rk = np.arange(1 << 16, dtype=np.int64) * 11 + 5
+    rp = np.arange(1 << 16, dtype=np.int64) - 9
+    n = 1 << 21
+    w = 1.0 / np.arange(1, 41) ** 0.9
+    hot = rng.choice(rk, 40, replace=False)
+    u = rng.random(n)
+    sk = np.where(u < 0.5, hot[rng.choice(40, n, p=w / w.sum())], rk[rng.integers(0, 1 << 16, n)]).astype(np.int64)
+    sp = np.arange(n, dtype=np.int64) * 3
+    o = run(hj, rk, rp, sk, sp, bits)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=4096))
+
+
 @pytest.mark.parametrize("bits", [3, 7])
 def test_radix_i32_many_matches_per_row(hj, oracle, bits):
     """~100 build copies per key (the reference's 10M x 10M / [1, 100k] shape,
