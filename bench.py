@@ -121,7 +121,9 @@ def cpu_baseline(seed, log2n):
         block scan -> staged probe) at H = |R|/100 (the reference's ratio,
         join-performances.md:3,8) and H = |R|, on all usable cores and on 1;
       * the nested loop (shared.cpp:154-165, nested-loop.mlir:29-192) up to
-        2^16 x 2^16, extrapolated quadratically to 2^28 x 2^28 (labelled)."""
+        2^16 x 2^16, extrapolated quadratically to 2^28 x 2^28 (labelled);
+      * the reference's own compiled check() (its nested loop + sort, kind
+        "reference") at 2^16 x 2^16 i32 on 1 core, when oracle/_ref is built."""
     sys.path.insert(0, ROOT)
     from oracle import pyoracle as O
     facts = host_facts()
@@ -161,12 +163,35 @@ def cpu_baseline(seed, log2n):
                                            "note": "quadratic extrapolation from the measured sample, not measured"}})
         return runs[-1]
 
+    def ref_nested(log2):
+        # the reference's OWN compiled CPU join: check() (shared.cpp:129-172,
+        # built from its sources into oracle/_ref/shared.so) runs the nested
+        # loop over i32 keys and compares its sorted pairs with ours
+        import numpy as np
+        n = 1 << log2
+        rng = np.random.default_rng(seed)
+        r = rng.permutation(n).astype(np.int32) + 1
+        ps = rng.permutation(n)
+        s = r[ps]
+        t0 = time.perf_counter()
+        ok = O.ref_check(r, s, ps.astype(np.int32), np.arange(n, dtype=np.int32))
+        dt = time.perf_counter() - t0
+        assert ok == 1, ok
+        ext = dt * (2.0 ** (28 - log2)) ** 2
+        runs.append({"algorithm": "reference check() nested loop (oracle/_ref/shared.so)", "kind": "reference",
+                     "rows": f"2^{log2} x 2^{log2} i32", "threads": 1, "seconds": round(dt, 3),
+                     "probe_tuples_per_s": round(n / dt, 1),
+                     "extrapolated_2p28": {"seconds": round(ext, 1), "probe_tuples_per_s": round((1 << 28) / ext, 2),
+                                           "note": "quadratic extrapolation from the measured sample, not measured"}})
+
     head = v2(log2n, 100, allc)                      # the headline: reference ratio, all cores
     v2(max(16, log2n - 2), 100, 1)                   # 1 core (bounded sample)
     v2(log2n, 1, allc)                               # H = |R|
     v2(log2n, 1, 1)
     nested(17, allc)
     nested(16, 1)
+    if O.ref_available():
+        ref_nested(16)
     return {"value": head["probe_tuples_per_s"], "unit": "probe tuples/s", "cores": allc, "kind": "port",
             "sample": f"join_v2 restated (oracle/hj_oracle.c), |R|=|S|=2^{log2n} PK-FK int64, H=|R|/100 "
                       f"(reference ratio), {allc} host threads; probe = count + probe phases "
