@@ -526,3 +526,57 @@ def test_radix_detect_many_suspects(hj, oracle, wide):
         assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
     assert hj.join_kernel == "k_join_b"
     assert hj.has_duplicates()
+
+
+def _fuzz_cases():
+    """Seeded sizes just around the kernels' units (64-row runs, 512/1024-row
+    buckets, 4096-row pass tiles, 8192-row probe chunks), key ranges from
+    every-key-repeats to nearly unique, both row widths, 1-3 pass plans."""
+    rng = np.random.default_rng(0x5eed)
+    units = [1, 63, 64, 65, 511, 513, 1023, 1025, 4095, 4096, 4097, 8191, 8193, 12289, 40961]
+    cases = []
+    for i in range(24):
+        nr = int(rng.choice(units)) + int(rng.integers(0, 3))
+        ns = int(rng.choice(units)) * int(rng.integers(1, 4))
+        span = int(rng.choice([3, 64, 1000, 1 << 20, 1 << 40]))
+        span = max(span, nr * ns // 2_000_000 + 1)   # at most ~2M result rows
+        bits = int(rng.choice([1, 4, 7, 9, 12, 17]))
+        wide = bool(i % 3)
+        cases.append((i, nr, ns, span if wide else min(span, 1 << 30), bits, wide))
+    return cases
+
+
+def _fuzz_keys(rng, lo, span, nr, ns):
+    # ~70 % of S rows take a key drawn from R (sparse spans still match)
+    rk = rng.integers(lo, lo + span, nr, dtype=np.int64)
+    sk = rng.integers(lo, lo + span, ns, dtype=np.int64)
+    hit = rng.random(ns) < 0.7
+    sk[hit] = rk[rng.integers(0, nr, int(hit.sum()))]
+    return rk, sk
+
+
+@pytest.mark.parametrize("i,nr,ns,span,bits,wide", _fuzz_cases())
+def test_radix_fuzz_ragged_vs_oracle(hj, oracle, i, nr, ns, span, bits, wide):
+    rng = np.random.default_rng(1000 + i)
+    lo = -span // 2
+    if wide:
+        rk, sk = _fuzz_keys(rng, lo, span, nr, ns)
+        rp = rng.integers(-(1 << 62), 1 << 62, nr, dtype=np.int64)
+        sp = rng.integers(-(1 << 62), 1 << 62, ns, dtype=np.int64)
+        exp = oracle.chained_join_i64(rk, rp, sk, sp, H=max(1, nr // 8))
+    else:
+        rk, sk = (a.astype(np.int32) for a in _fuzz_keys(rng, lo, span, nr, ns))
+        rp = sp = None
+        exp = oracle.chained_join_i32(rk, sk, H=max(1, nr // 8))
+    o = run(hj, rk, rp, sk, sp, bits)
+    assert len(o[0]) == len(exp[0])
+    assert oracle.same_multiset(*o, *exp)
+    if i % 4 == 0:   # the same inputs through the global (one HBM table) strategy
+        hj.set_strategy("global")
+        try:
+            g_r, g_s = hj.join(dev(rk), None if rp is None else dev(rp), dev(sk), None if sp is None else dev(sp))
+            assert hj.strategy_used == "global"
+            torch.cuda.synchronize()
+        finally:
+            hj.set_strategy("auto")
+        assert oracle.same_multiset(g_r.cpu().numpy().astype(np.int64), g_s.cpu().numpy().astype(np.int64), *exp)
