@@ -88,12 +88,6 @@ int hj_ctx_set_strategy(hj_ctx *ctx, int strategy);
 /* RADIX: partition into exactly 2^bits partitions (1..24; 0 = planner's
  * choice, ~4096 build rows per partition).  For tests and tuning. */
 int hj_ctx_set_radix_bits(hj_ctx *ctx, int bits);
-/* GLOBAL probes of tables larger than one XCD's L2 (4 MiB .. 128 MiB) and
- * probe sides >= 2^22 rows first split the probe rows into 8 groups by the
- * table's top slot bits, so each XCD probes 1/8 of the table from its own L2.
- * mode: -1 automatic (default; env HJ_XCD=0/1 overrides -- automatic is
- * currently "never"), 0 never, 1 always. */
-int hj_ctx_set_xcd_split(hj_ctx *ctx, int mode);
 /* Strategy of the last probe since the current build (else of the build):
  * HJ_STRATEGY_GLOBAL / _RADIX, 0 if none.  Under HJ_STRATEGY_AUTO a build side
  * of [2^18, 2^21) rows gets the global table AND a radix partition; a probe

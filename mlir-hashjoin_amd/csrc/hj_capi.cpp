@@ -118,7 +118,6 @@ struct hj_ctx {
     int64_t n_build = 0;
     int strategy = HJ_STRATEGY_AUTO;   // requested
     int radix_bits = 0;                // 0: planner chooses
-    int xcd_mode = -1;                 // global-table probe XCD split: -1 auto, 0 off, 1 on
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
     bool dual = false;                 // global build whose R is ALSO radix-partitioned (probe-time choice)
     int probe_used = -1;               // strategy of the last probe (-1: none since the build)
@@ -168,12 +167,7 @@ struct hj_ctx {
     // follows from these and the build-time sample in meta[2..3])
     bool join_ran = false, join_wide = false, join_stream = false;
     bool routed = false;   // the current build came from hj_dev_build_routed_i64 (plan.skip owner bits)
-    hipStream_t join_st = nullptr;
-    // ... and its R view and partition count, for the on-demand repeat check
-    // (hj_ctx_build_has_duplicates); join_checked: that check ran for it
-    hj::BucketSet join_r{};
-    int join_nparts = -1;
-    bool join_checked = false;
+    bool dup_checked = false;   // hj_ctx_build_has_duplicates ran its DETECT build for this build
 };
 
 namespace {
@@ -328,6 +322,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->used = choose_strategy(c, src.n);
     c->probe_used = -1;
     c->join_ran = false;
+    c->dup_checked = false;
     c->routed = false;
     c->memo.valid = false;   // (hj_count_*'s kept table is gone)
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
@@ -365,38 +360,6 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     return HJ_OK;
 }
 
-// XCD split of a global-table probe: worth its extra pass when the table is
-// larger than one XCD's 4 MiB L2 but small enough that 1/8 of it mostly fits
-// (<= 128 MiB), and the probe side is large.  HJ_XCD=0 / 1 forces it off / on.
-constexpr size_t kXcdMinTable = 4ull << 20, kXcdMaxTable = 128ull << 20;
-constexpr int64_t kXcdMinRows = 1ll << 22;
-
-hj::RadixPlan xcd_plan() {
-    hj::RadixPlan pl{};
-    pl.passes = 1;
-    pl.bits[0] = 3;   // log2(kXcdGroups)
-    pl.pbl[0] = hj::kXcdPbl;
-    pl.total_bits = 3;
-    return pl;
-}
-
-bool use_xcd_split(const hj_ctx *c, int layout, int64_t n) {
-    static const int env = [] {
-        const char *e = getenv("HJ_XCD");
-        return e ? atoi(e) : -1;
-    }();
-    const int mode = c->xcd_mode >= 0 ? c->xcd_mode : env;
-    if (mode == 0 || n <= 0) return false;
-    if (mode == 1) return true;
-    // automatic: off for now -- the split cuts the probe's fetched bytes 3.4x
-    // (L2 hit 0.24 -> 0.73 at C2) but the probe kernel is bound elsewhere
-    // (row-list indirection + output cursor), so C2 measured 31.1 ms split vs
-    // 26.6 ms plain (profiles/r01_c2_xcd_profile.txt)
-    if (mode < 0) return false;
-    const size_t table = (size_t(1) << c->bits) * (layout == kWide ? 16 : 8);
-    return n >= kXcdMinRows && table > kXcdMinTable && table <= kXcdMaxTable;
-}
-
 int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *out_s, int64_t cap,
              uint64_t *d_count, bool count_only, hipStream_t st) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
@@ -427,11 +390,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         c->join_ran = true;
         c->join_wide = wide;
         c->join_stream = stream;
-        c->join_st = st;
-        c->join_r = bucket_set(c->rset);
-        c->join_nparts = -1;
-        c->join_checked = false;
-        trace("probe: joined", st, cap);
+            trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
         c->rec_mid = c->timing;
@@ -444,31 +403,6 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     out.counter = (unsigned long long *)d_count;
     record(c, kEvProbe0, st);
     size_t slow_cap = hj::probe_tiles(src.n);
-    if (use_xcd_split(c, layout, src.n)) {
-        // XCD split: route S by the top 3 bits of the slot hash into 8 groups
-        // (one bucket-chaining pass), then workgroup b probes group b % 8 --
-        // its 1/8 of the table stays in one XCD's L2
-        // (profiles/r01_micro_xcd_slices.txt: 66 -> 265 G probes/s at 32 MiB)
-        const bool wide = layout == kWide;
-        const hj::RadixPlan pl = xcd_plan();
-        HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, wide ? 16 : 8, pl));
-        const size_t xcap = hj::probe_tiles_xcd(c->sset.max_runs);
-        if (xcap > slow_cap) slow_cap = xcap;
-        HJ_TRY(ensure_buf(c->slow, slow_cap * sizeof(unsigned)));
-        HJ_HIP(hj::radix_partition(src, wide, pl, radix_work(c), bucket_set(c->sset), st));
-        record(c, kEvProbeMid, st);
-        hj::SrcDev xs = src;
-        xs.key = c->sset.rows.p;
-        xs.pay = nullptr;
-        xs.form = hj::kXcdRows;
-        xs.runs = (const unsigned long long *)c->sset.runs.p;
-        xs.rstart = (const unsigned long long *)c->sset.rstart.p;
-        HJ_HIP(hj::launch_probe(table_dev(c), layout, xs, out, count_only, (unsigned *)c->slow.p, slow_cap, st));
-        record(c, kEvProbe1, st);
-        c->rec[2] = c->timing;
-        c->rec_mid = c->timing;
-        return HJ_OK;
-    }
     HJ_TRY(ensure_buf(c->slow, slow_cap * sizeof(unsigned)));
     HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, (unsigned *)c->slow.p, slow_cap, st));
     record(c, kEvProbe1, st);
@@ -1091,18 +1025,16 @@ int hj_ctx_build_has_duplicates(hj_ctx *c) {
     unsigned long long v = 0;
     HJ_HIP(hipDeviceSynchronize());
     HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
-    if (!v && c->join_ran && !c->join_checked) {
-        // k_join_b flags only the repeats its probe rows met: the rest of the
-        // answer, once per join (its items' work map is still resident)
-        unsigned long long smp[2] = {0, 0};
-        HJ_HIP(hipMemcpy(smp, c->meta + 2, sizeof(smp), hipMemcpyDeviceToHost));
-        if (hj::join_kernel_choice(c->join_wide, c->join_stream, smp[0], smp[1]) == HJ_JOIN_KERNEL_BUCKETED) {
-            HJ_HIP(hj::radix_detect(c->join_wide, c->plan, c->join_r, (const unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1,
-                                    c->meta + 2, c->join_nparts, c->join_st));
-            HJ_HIP(hipDeviceSynchronize());
-            HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
-        }
-        c->join_checked = true;
+    if (!v && c->used == HJ_STRATEGY_RADIX && !c->dup_checked) {
+        // the joins flag only the repeats of partitions they built (k_join_b:
+        // only those a probe row met): the exact answer, once per build, is a
+        // DETECT build over every partition of R (the work map is rebuilt from
+        // R alone; the last join's map is not needed again)
+        HJ_HIP(hj::radix_detect(c->layout == kWide, c->plan, radix_work(c), bucket_set(c->rset),
+                                (unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1, c->meta + 2, nullptr));
+        HJ_HIP(hipDeviceSynchronize());
+        HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
+        c->dup_checked = true;
     }
     return v ? 1 : 0;
 }
@@ -1176,12 +1108,6 @@ int hj_ctx_set_radix_bits(hj_ctx *c, int bits) {
     return HJ_OK;
 }
 
-int hj_ctx_set_xcd_split(hj_ctx *c, int mode) {
-    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
-    if (mode < -1 || mode > 1) HJ_FAIL(HJ_ERR_ARG, "mode must be -1, 0 or 1");
-    c->xcd_mode = mode;
-    return HJ_OK;
-}
 
 int hj_ctx_strategy_used(const hj_ctx *c) {
     if (!c || c->layout < 0) return 0;
@@ -1311,6 +1237,7 @@ int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->memo.valid = false;
     c->plan = pl;
     c->routed = true;
+    c->dup_checked = false;
     HJ_TRY(ensure_radix_scratch(c, c->rset, n, 16, pl));
     record(c, kEvInit0, st);
     HJ_HIP(hipMemsetAsync(c->meta, 0, 4 * sizeof(unsigned long long), st));
@@ -1355,10 +1282,6 @@ int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->join_ran = true;
     c->join_wide = true;
     c->join_stream = stream_shape;
-    c->join_st = st;
-    c->join_r = r;
-    c->join_nparts = nbins << c->plan.bits[1];
-    c->join_checked = false;
     record(c, kEvProbe1, st);
     c->rec[2] = c->timing;
     c->rec_mid = c->timing;

@@ -85,23 +85,16 @@ struct TableDev {
 
 enum Layout : int { kWide = 0, kNarrow = 1 };
 
-// Source forms of a relation on the device.  kXcdRows: a probe side already
-// split into 8 groups by the top 3 bits of the table's slot hash (a radix
-// bucket set of 512-row buckets, packed rows as the partition passes write
-// them), probed group g by workgroups b with b % 8 == g.
-enum SrcForm : int { kCols64 = 0, kPacked64 = 1, kCol32 = 2, kXcdRows = 5 };
+// Source forms of a relation on the device.
+enum SrcForm : int { kCols64 = 0, kPacked64 = 1, kCol32 = 2 };
 
 struct SrcDev {
-    const void *key;    // int64 column, packed {key,pay} tuples, int32 column, or bucket rows (kXcdRows)
+    const void *key;    // int64 column, packed {key,pay} tuples or int32 column
     const void *pay;    // int64 column (kCols64 only)
     long long n;
     long long row_base; // kCol32: row id = row_base + row
     int form;
-    const unsigned long long *runs = nullptr;     // kXcdRows: runs (row << 7 | count), grouped
-    const unsigned long long *rstart = nullptr;   // kXcdRows: 9 group starts into runs
 };
-constexpr int kXcdPbl = 9;        // rows per bucket of a kXcdRows probe side (log2)
-constexpr int kXcdGroups = 8;     // one per XCD
 
 struct OutDev {
     void *r;            // int64 or int32 column (R payload / row id)
@@ -117,11 +110,9 @@ hipError_t launch_build(const TableDev &t, int layout, const SrcDev &src, hipStr
 // count lives in meta[3])
 size_t probe_tiles(long long n);
 // slow_cap: entries of `slow` (tiles beyond it are never written; the
-// callers size it from probe_tiles / probe_tiles_xcd so that cannot happen)
+// callers size it from probe_tiles so that cannot happen)
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
                         bool count_only, unsigned *slow, size_t slow_cap, hipStream_t st);
-// slow-list entries an XCD-grouped probe side of max_runs runs can need
-size_t probe_tiles_xcd(unsigned long long max_runs);
 
 // ---------------------------------------------------------------- radix join
 // (hj_radix.hip) partitions both relations by the top bits of the key hash
@@ -221,12 +212,14 @@ hipError_t radix_partition_routed(const void *tuples, long long n, const unsigne
 // the caller).  Deterministic for given data.
 hipError_t radix_sample(bool wide, const RadixPlan &pl, const BucketSet &r, unsigned long long *sample,
                         hipStream_t st);
-// The exact "build keys repeat" answer for the items of the last radix_join
-// (work_start / desc as it left them, same r view and nparts) that k_join_b
-// joined: its DETECT build, setting *dup_flag.  (k_join_b only flags repeats a
-// probe row met; the other join kernels answer exactly during the join.)
-hipError_t radix_detect(bool wide, const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
-                        unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st);
+// The exact "build keys repeat" answer for the whole build side r (the
+// plan's 2^total_bits partitions): k_join_b's DETECT build over one item per
+// non-empty partition (a work map rebuilt from r.rstart alone, in work_start /
+// desc), the partitions it cannot take by k_join's list-mode build (repeats
+// inside each of its build rounds); sets *dup_flag.  The joins themselves only
+// flag repeats of partitions they built (k_join_b: that a probe row met).
+hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, unsigned *work_start,
+                        void *desc, unsigned long long *dup_flag, const unsigned long long *sample, hipStream_t st);
 // HJ_JOIN_KERNEL_* of the radix join for this shape and sample (host mirror
 // of the device-side choice)
 int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned long long repeats);

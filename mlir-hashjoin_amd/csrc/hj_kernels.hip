@@ -168,53 +168,15 @@ __global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
 }
 
 // ------------------------------------------------------------------ probe tiles
-// A probe tile is kProbeItems * kBlock rows.  Plain sources: tile q = rows
-// [q * kTile, ...).  kXcdRows: tile (g, q) = runs 32q .. 32q+31 of group g.
+// A probe tile is kProbeItems * kBlock rows: tile q = rows [q * kTile, ...).
 constexpr int kProbeTile = kBlock * kProbeItems;
-constexpr int kXcdTileRuns = kProbeTile >> kRunLog;
-static_assert(kXcdTileRuns * (1 << kRunLog) == kProbeTile, "tile = whole runs");
 
 template <int L, int FORM>
-__device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned g, unsigned long long q, int i, Tuple &tp) {
-    if constexpr (FORM == kXcdRows) {
-        const unsigned v = (unsigned)i * kBlock + threadIdx.x;
-        const unsigned long long li = src.rstart[g] + q * kXcdTileRuns + (v >> kRunLog);
-        if (li >= src.rstart[g + 1]) return false;
-        const unsigned long long e = src.runs[li];
-        const unsigned off = v & ((1u << kRunLog) - 1u);
-        if (off >= (unsigned)(e & 127u)) return false;
-        const unsigned long long r = (e >> 7) + off;
-        if constexpr (L == kWide) {
-            const ulonglong2 x = ((const ulonglong2 *)src.key)[r];
-            tp = Tuple{x.x, x.y};
-        } else {
-            const unsigned long long x = ((const unsigned long long *)src.key)[r];
-            tp = Tuple{x >> 32, x & 0xffffffffull};
-        }
-        return true;
-    } else {
-        const long long row = (long long)q * kProbeTile + (long long)i * kBlock + threadIdx.x;
-        if (row >= src.n) return false;
-        tp = load_src<FORM>(src, row);
-        return true;
-    }
-}
-
-// Tiles of this workgroup: (group, first tile, stride, tile count).
-template <int FORM>
-__device__ __forceinline__ void probe_tiles(const SrcDev &src, unsigned &g, unsigned long long &q0,
-                                            unsigned long long &step, unsigned long long &nt) {
-    if constexpr (FORM == kXcdRows) {
-        g = blockIdx.x % kXcdGroups;   // round-robin block -> XCD deal: group g stays in one XCD's L2
-        q0 = blockIdx.x / kXcdGroups;
-        step = gridDim.x / kXcdGroups;
-        nt = (src.rstart[g + 1] - src.rstart[g] + kXcdTileRuns - 1) / kXcdTileRuns;
-    } else {
-        g = 0;
-        q0 = blockIdx.x;
-        step = gridDim.x;
-        nt = (unsigned long long)((src.n + kProbeTile - 1) / kProbeTile);
-    }
+__device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned long long q, int i, Tuple &tp) {
+    const long long row = (long long)q * kProbeTile + (long long)i * kBlock + threadIdx.x;
+    if (row >= src.n) return false;
+    tp = load_src<FORM>(src, row);
+    return true;
 }
 
 // ------------------------------------------------------------------ probe
@@ -253,17 +215,15 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
     const slot_t *sl = (const slot_t *)t.slots;
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    unsigned g;
-    unsigned long long q0, step, nt;
-    probe_tiles<FORM>(src, g, q0, step, nt);
-    for (unsigned long long q = q0; q < nt; q += step) {
+    const unsigned long long nt = (unsigned long long)((src.n + kProbeTile - 1) / kProbeTile);
+    for (unsigned long long q = blockIdx.x; q < nt; q += gridDim.x) {
         unsigned long long K[kProbeItems], P[kProbeItems];
         bool V[kProbeItems];
         bool has_null = false;
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
             Tuple tp{0ull, 0ull};
-            V[i] = probe_row<L, FORM>(src, g, q, i, tp);
+            V[i] = probe_row<L, FORM>(src, q, i, tp);
             K[i] = tp.k;
             P[i] = tp.p;
             has_null |= V[i] && LY::null_key(K[i]);
@@ -272,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
             // general path: k_probe_slow takes this tile
             if (threadIdx.x == 0) {
                 const unsigned long long j = atomicAdd(&t.meta[3], 1ull);
-                if (j < slow_cap) slow[j] = (unsigned)(q * kXcdGroups + g);   // (sized so it always is; else k_probe_slow flags the count)
+                if (j < slow_cap) slow[j] = (unsigned)q;   // (sized so it always is; else k_probe_slow flags the count)
             }
             continue;
         }
@@ -383,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_slow(TableDev t, SrcDev src, O
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
             Tuple tp{0ull, 0ull};
-            V[i] = probe_row<L, FORM>(src, id % kXcdGroups, id / kXcdGroups, i, tp);
+            V[i] = probe_row<L, FORM>(src, id, i, tp);
             K[i] = tp.k;
             P[i] = tp.p;
         }
@@ -945,12 +905,6 @@ size_t probe_tiles(long long n) {
     return (size_t)(n > 0 ? (n + kProbeTile - 1) / kProbeTile : 0) + 1;
 }
 
-size_t probe_tiles_xcd(unsigned long long max_runs) {
-    // XCD-group tiles: group g has ceil(runs_g / kXcdTileRuns) tiles, and the
-    // runs of all groups fit the set's run list (max_runs entries)
-    return (size_t)(max_runs / kXcdTileRuns) + kXcdGroups + 1;
-}
-
 hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const OutDev &out,
                         bool count_only, unsigned *slow, size_t slow_cap, hipStream_t st) {
     if (src.n <= 0) return hipSuccess;
@@ -960,9 +914,7 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned tiles = grid_for(src.n, kProbeTile);
-    // plain: one block per tile; XCD groups: a strided grid, a multiple of 8,
-    // 20 workgroups per CU (C2 sweep 4/5/10/20: 20 is fastest)
-    const unsigned g = src.form == kXcdRows ? (unsigned)(cus * 20) / kXcdGroups * kXcdGroups : tiles;
+    const unsigned g = tiles;   // one block per tile
     const unsigned gs = tiles < (unsigned)(cus * 8) ? tiles : (unsigned)(cus * 8);
 #define HJ_PROBE(L, F)                                                                                        \
     do {                                                                                                      \
@@ -979,11 +931,9 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
     if (layout == kWide) {
         if (src.form == kCols64) HJ_PROBE(kWide, kCols64);
         else if (src.form == kPacked64) HJ_PROBE(kWide, kPacked64);
-        else if (src.form == kXcdRows) HJ_PROBE(kWide, kXcdRows);
         else return hipErrorInvalidValue;
     } else {
         if (src.form == kCol32) HJ_PROBE(kNarrow, kCol32);
-        else if (src.form == kXcdRows) HJ_PROBE(kNarrow, kXcdRows);
         else return hipErrorInvalidValue;
     }
 #undef HJ_PROBE

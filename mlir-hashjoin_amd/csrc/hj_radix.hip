@@ -51,11 +51,9 @@ constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build 
 constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
 constexpr int kBucketed = 4;       // SrcForm of a previous pass's bucket set
 constexpr unsigned kNoBucket = 0xFFFFFFFFu;
-// Join items of multi-chunk partitions first (k_item_desc); 0 = partition order.
-#ifndef HJ_HEAVY_FIRST
-#define HJ_HEAVY_FIRST 1
-#endif
-constexpr bool kHeavyFirst = HJ_HEAVY_FIRST != 0;
+// Join items of multi-chunk partitions first (k_item_desc): int64 rows only
+// (profiles/r03_heavy_first.txt).
+constexpr bool kHeavyFirst = true;
 constexpr int kPassPbl = 10;       // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return radix_hash(k); }
@@ -82,11 +80,9 @@ struct Row<false> {   // i32 key (zero-extended) / i32 row id, packed key << 32 
     static __device__ __forceinline__ T zero() { return 0ull; }
 };
 
-// Streaming (non-temporal) loads/stores for data touched once per kernel:
-// HJ_NT bit 1 pass loads, 2 pass stores, 4 join loads, 8 join stores.
-#ifndef HJ_NT
-#define HJ_NT 12   // measured: join loads + stores nt -2.7 % (profiles/r01_nt_variants.txt); pass stores nt +66 %, pass loads nt +3 %
-#endif
+// Streaming (non-temporal) loads/stores for data touched once per kernel.
+// Measured (profiles/r01_nt_variants.txt): join loads + stores nt -2.7 %;
+// pass stores nt +66 % (they defeat the L2's line assembly), pass loads nt +3 %.
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 template <bool NT, typename T>
 __device__ __forceinline__ T ld_s(const T *p) {
@@ -115,8 +111,8 @@ __device__ __forceinline__ void st_s(T *p, const T &v) {
         __builtin_nontemporal_store(v, p);
     }
 }
-constexpr bool kNtPassLd = (HJ_NT & 1) != 0, kNtPassSt = (HJ_NT & 2) != 0;
-constexpr bool kNtJoinLd = (HJ_NT & 4) != 0, kNtJoinSt = (HJ_NT & 8) != 0;
+constexpr bool kNtPassLd = false, kNtPassSt = false;
+constexpr bool kNtJoinLd = true, kNtJoinSt = true;
 
 // Row `row` of a pass input in form FORM.
 template <bool WIDE, int FORM>
@@ -918,6 +914,8 @@ struct JoinArgs {
     // by this counter (zeroed by k_item_desc) instead of w += grid, so
     // workgroups that drew heavy items (a hot key's chunks) take fewer
     unsigned *next_item = nullptr;
+    // k_join (radix_detect): build only -- every item's S chunk is empty
+    bool empty_s = false;
 };
 
 constexpr unsigned kModeUnique = 1u, kModeSome = 2u, kModeMostlyRepeated = 4u;
@@ -1071,8 +1069,9 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
     auto item = [&](unsigned x) {
-        if constexpr (LIST) return a.desc[a.list[x]];
-        else return a.desc[x];
+        ItemDesc d = LIST ? a.desc[a.list[x]] : a.desc[x];
+        if (a.empty_s) d.s_hi = d.s_lo;
+        return d;
     };
 
     // Row slot i of wave v is run lo + i * NW + v, lane l its row l: the
@@ -2005,7 +2004,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             if (!DETECT) ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
         }
         if (!fits) {
-            if (!DETECT && threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+            // (DETECT: to k_join's list-mode build, which flags repeats)
+            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             if (dyn) {   // (every thread has read s_next above; the claim is read next iteration)
                 __syncthreads();
                 if (threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
@@ -2096,8 +2096,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
             if (bad) s_bad = 1u;
             __syncthreads();
             if (s_bad) {
-                // (DETECT: the item went to k_join, whose build flagged repeats)
-                if (!DETECT && threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
+                // (DETECT: as well -- to k_join's list-mode build)
+                if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             } else if constexpr (DETECT) {
                 // ---- the exact "build keys repeat" answer: each suspect walks
                 // its chain (home bucket, then on while a bucket's count says a
@@ -2572,46 +2572,16 @@ constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 3, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
-// i32 rows: threads, build / probe rows per thread, waves per SIMD,
-// workgroups per CU, table slots (log2) and the plan's partition size (log2
-// of twice the average build rows); HJ_NARROW_BKT: the bucketed k_join_b (else
-// k_join_u).  HJ_NARROW_SHAPE picks another for experiment builds (make
-// EXTRA=-DHJ_NARROW_SHAPE=n).  REF-B's join (profiles/r03_narrow_shapes.txt):
-// k_join_u over 8192 slots (shape 4, the round-3 start) 1.16 ms; k_join_b
-// over 4096 slots: 768 x 3+3 0.92 ms (shape 7), 512 x 5+4 at 3 per CU 0.96,
-// 512 x 5+3 at 4 per CU 1.35 and 1024 x 3+3 1.12 (both spill at the 64-VGPR
-// cap); k_join_b over 8192 slots (keys + row ids 64 KiB, partitions of ~3000
-// rows: half the items): 768 x 3+3 0.886 (shape 6), 768 x 4+4 0.779
-// (product); 4+6 and 5+5 spill.
-#ifndef HJ_NARROW_SHAPE
-#define HJ_NARROW_SHAPE 0
-#endif
-#if HJ_NARROW_SHAPE == 1
-constexpr int kNarrowNT = 512, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 8, kNarrowPerCU = 4, kTableLogNarrow = 12,
-              kPlanLogNarrow = 12;
-#define HJ_NARROW_BKT 0
-#elif HJ_NARROW_SHAPE == 4
-constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
-              kPlanLogNarrow = 13;
-#define HJ_NARROW_BKT 0
-#elif HJ_NARROW_SHAPE == 5
-constexpr int kNarrowNT = 512, kNarrowRI = 5, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 3, kTableLogNarrow = 12,
-              kPlanLogNarrow = 12;
-#define HJ_NARROW_BKT 1
-#elif HJ_NARROW_SHAPE == 6
-constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
-              kPlanLogNarrow = 13;
-#define HJ_NARROW_BKT 1
-#elif HJ_NARROW_SHAPE == 7
-constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 3, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 12,
-              kPlanLogNarrow = 12;
-#define HJ_NARROW_BKT 1
-
-#else
+// i32 rows: k_join_b over 8192 slots (keys and row ids apart: 64 KiB), 768
+// threads x 4 build + 4 probe rows, 6 waves per SIMD, 2 workgroups per CU;
+// plan partitions of ~4096 rows (log2 of twice the average build rows).
+// REF-B's join (profiles/r03_narrow_shapes.txt; the other shapes live on in
+// micro/ only): k_join_u over 8192 slots 1.16 ms; k_join_b over 4096 slots
+// 768 x 3+3 0.92, 512 x 5+4 at 3 per CU 0.96, 512 x 5+3 at 4 per CU 1.35 and
+// 1024 x 3+3 1.12 (both spill at the 64-VGPR cap); over 8192 slots 768 x 3+3
+// 0.886, 768 x 4+4 0.779 (this shape); 4+6 and 5+5 spill.
 constexpr int kNarrowNT = 768, kNarrowRI = 4, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
               kPlanLogNarrow = 13;
-#define HJ_NARROW_BKT 1
-#endif
 
 int cu_count() {
     static int n = [] {
@@ -3084,7 +3054,6 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         a.modes = kModeUnique | kModeSome;
         {
             const unsigned gn = items < pgn ? items : pgn;
-#if HJ_NARROW_BKT
             a.next_item = next_item;
             if (count_only)
                 hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS, false,
@@ -3095,14 +3064,6 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                                              kTableLogNarrow>),
                                    dim3(gn), dim3(kNarrowNT), 0, st, a);
             a.next_item = nullptr;
-#else
-            if (count_only)
-                hipLaunchKernelGGL((k_join_u<false, false, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
-                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
-            else
-                hipLaunchKernelGGL((k_join_u<false, true, kTableLogNarrow, kNarrowNT, kNarrowRI, kNarrowSI, kNarrowWPS>),
-                                   dim3(gn), dim3(kNarrowNT), 0, st, a);
-#endif
         }
         a.list = defer_n + 1;
         a.list_n = defer_n;
@@ -3128,32 +3089,58 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     return hipGetLastError();
 }
 
-hipError_t radix_detect(bool wide, const RadixPlan &pl, const BucketSet &r, const unsigned *work_start, const void *desc,
-                        unsigned long long *dup_flag, const unsigned long long *sample, int nparts, hipStream_t st) {
-    // over the last join's items (work map and descriptors still resident):
-    // the items k_join_b built -- the others' kernels answered during the join
+hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, unsigned *work_start,
+                        void *desc, unsigned long long *dup_flag, const unsigned long long *sample, hipStream_t st) {
+    // one item per non-empty partition of the WHOLE build side (a work map
+    // from r.rstart alone: partitions no probe row reached are checked too)
+    const int P = 1 << pl.total_bits;
+    unsigned *work_owner = work_start + P + 1;
+    const unsigned whole = 0x7FFFFFFFu;   // runs per item: a partition is one item
+    chunk_map(r.rstart, r.rstart, P, whole, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    unsigned *defer_n = work_owner + radix_join_items(pl, 0);
+    hipLaunchKernelGGL(k_item_desc, dim3(blocks_for((u64)P + 1, 256)), dim3(256), 0, st, (const unsigned *)work_start,
+                       (const unsigned *)work_owner, (const u64 *)r.rstart, (const u64 *)r.rstart, P, whole,
+                       (ItemDesc *)desc, defer_n, nullptr, nullptr, nullptr);
     JoinArgs a{};
     a.r = r.rows;
+    a.s = r.rows;
     a.r_runs = r.runs;
+    a.s_runs = r.runs;
     a.r_rstart = r.rstart;
-    a.P = nparts >= 0 ? nparts : 1 << pl.total_bits;
+    a.s_rstart = r.rstart;
+    a.P = P;
     a.work_start = work_start;
     a.desc = (const ItemDesc *)desc;
     a.tshift = 64 - pl.skip - pl.total_bits - (wide ? kTableLog : kTableLogNarrow);
     a.dup_flag = dup_flag;
     a.sample = sample;
-    a.modes = kModeUnique | kModeSome;
+    a.modes = kModesAll;
+    // partitions the bucketed table cannot take (oversized) are deferred to
+    // k_join's list-mode build below, which flags repeats inside each of its
+    // build rounds
+    a.defer = defer_n + 1;
+    a.defer_n = defer_n;
     if (wide)
         hipLaunchKernelGGL((k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS, true>), dim3(2 * cu_count()),
                            dim3(kFastNT), 0, st, a);
-#if HJ_NARROW_BKT
     else
         // (its signature words and suspect list on top of the table: one
         // workgroup per CU at 8192 slots: 3 waves per SIMD, register budget as for 4)
         hipLaunchKernelGGL((k_join_b<false, false, kNarrowNT, kNarrowRI, kNarrowSI, (kTableLogNarrow > 12 ? 3 : kNarrowWPS),
                                      true, kTableLogNarrow>),
                            dim3(kNarrowPerCU * cu_count()), dim3(kNarrowNT), 0, st, a);
-#endif
+    // the deferred partitions: k_join builds them (its probe sees an empty S
+    // chunk: an item's S runs are [s_lo, s_lo) below)
+    a.list = defer_n + 1;
+    a.list_n = defer_n;
+    a.empty_s = true;
+    a.counter = ws.pcur;   // (no probe rows: nothing is counted; a valid word all the same)
+    if (wide)
+        hipLaunchKernelGGL((k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
+                           dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_join<false, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
+                           dim3(512), 0, st, a);
     return hipGetLastError();
 }
 
@@ -3174,7 +3161,7 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
         if (stream) return HJ_JOIN_KERNEL_STREAM;
         return m == 2 ? HJ_JOIN_KERNEL_LINEAR : HJ_JOIN_KERNEL_BUCKETED;
     }
-    return m == 2 ? HJ_JOIN_KERNEL_GROUPED : (HJ_NARROW_BKT ? HJ_JOIN_KERNEL_BUCKETED : HJ_JOIN_KERNEL_LINEAR);
+    return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_BUCKETED;
 }
 
 }  // namespace hj

@@ -64,7 +64,6 @@ def _load():
         "hj_ctx_set_strategy": (_int, [_vp, _int]),
         "hj_ctx_strategy_used": (_int, [_vp]),
         "hj_ctx_set_radix_bits": (_int, [_vp, _int]),
-        "hj_ctx_set_xcd_split": (_int, [_vp, _int]),
         "hj_dev_build_i64": (_int, [_vp, _vp, _vp, _i64, _vp]),
         "hj_dev_count_i64": (_int, [_vp, _vp, _i64, _vp, _vp]),
         "hj_dev_probe_i64": (_int, [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp]),

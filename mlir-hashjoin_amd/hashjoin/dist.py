@@ -256,6 +256,16 @@ def all_gather_rows(tuples, group=None):
     return torch.cat([full[p * mx:p * mx + counts[p]] for p in range(world)])
 
 
+def _checked_count(cnt):
+    """The match count a probe returned; bit 63 set (a negative int64) means
+    an internal work list overflowed and the pairs are incomplete (hj.h), so
+    it is an error, never a row count (as in HashJoin.join)."""
+    m = int(cnt.item())
+    if m < 0:
+        raise RuntimeError("hash join: internal work list overflow (count flagged)")
+    return m
+
+
 def _probe_all(hj, tuples, capacity, probe=None):
     """Probe into an output sized optimistically, once more at the exact M.
     probe(tuples, out_r, out_s) -> count tensor (default hj.probe_tuples)."""
@@ -264,8 +274,7 @@ def _probe_all(hj, tuples, capacity, probe=None):
     for _ in range(2):
         out_r = torch.empty(cap, dtype=torch.int64, device=tuples.device)
         out_s = torch.empty(cap, dtype=torch.int64, device=tuples.device)
-        cnt = probe(tuples, out_r, out_s)
-        m = int(cnt.item())
+        m = _checked_count(probe(tuples, out_r, out_s))
         if m <= cap:
             return out_r[:m], out_s[:m]
         cap = m
@@ -289,7 +298,7 @@ def _probe_parts(hj, parts, capacity, total, device, probes=None):
             continue
         m = None
         if cap > pos:
-            m = int(probe(t, out_r[pos:], out_s[pos:]).item())
+            m = _checked_count(probe(t, out_r[pos:], out_s[pos:]))
             if m <= cap - pos:
                 pos += m
                 continue

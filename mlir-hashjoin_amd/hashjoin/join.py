@@ -78,12 +78,6 @@ class HashJoin:
         check(lib.hj_ctx_set_strategy(self._ctx, STRATEGIES[name]), "hj_ctx_set_strategy")
         check(lib.hj_ctx_set_radix_bits(self._ctx, int(radix_bits)), "hj_ctx_set_radix_bits")
 
-    def set_xcd_split(self, mode):
-        """Global-table probe split by XCD: None/'auto', True (always), False (never)."""
-        m = -1 if mode in (None, "auto") else (1 if mode else 0)
-        check(lib.hj_ctx_set_xcd_split(self._ctx, m), "hj_ctx_set_xcd_split")
-
-    @property
     def strategy_used(self):
         return {HJ_STRATEGY_GLOBAL: "global", HJ_STRATEGY_RADIX: "radix"}.get(
             lib.hj_ctx_strategy_used(self._ctx), None)

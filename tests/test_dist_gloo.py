@@ -17,6 +17,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# a rank that never reaches its rendezvous (e.g. a port taken between
+# _free_port and init) must fail the test, not hang the suite
+pytestmark = pytest.mark.timeout(300, method="thread")
 
 
 def _free_port():
@@ -105,11 +108,14 @@ def test_two_rank_exchange_join(case, tmp_path, oracle):
 class _CpuJoin:
     """HashJoin's partition / build_tuples / probe_tuples on CPU tensors."""
 
-    def __init__(self):
+    def __init__(self, flag=False, plan=None):
         from oracle import pyoracle as O
         self.O = O
         self.r = None
         self.calls = {"partition": 0, "build": 0, "probe": 0}
+        self.flag = flag   # probes return a count with bit 63 set (work list overflowed)
+        if plan is not None:   # the library's own folded-routing plan (host function, no GPU)
+            self.route_plan = plan
 
     def partition(self, key, pay, nparts):
         self.calls["partition"] += 1
@@ -169,6 +175,8 @@ class _CpuJoin:
         k = min(m, out_r.numel())
         out_r[:k] = torch.from_numpy(o_r[:k])
         out_s[:k] = torch.from_numpy(o_s[:k])
+        if self.flag:
+            return torch.tensor([m | -(1 << 63)], dtype=torch.int64)
         return torch.tensor([m], dtype=torch.int64)
 
 
@@ -194,8 +202,29 @@ def _dj_worker(rank, world, port, case, outdir):
     from hashjoin.dist import distributed_join
     from test_abi import _np_partition_of
     rk, rp, sk, sp = (torch.from_numpy(x) for x in _relations(case, rank, world))
-    hj = _CpuJoin()
+    plan = None
+    if case.get("plan_n"):
+        # the N = 8 product plan: hj_route_plan for the bench's global |R|
+        # (2^28 over 8 ranks -> 6 bins per owner), applied to small relations
+        import hashjoin
+        sub = hashjoin.HashJoin.route_plan(case["plan_n"], world)
+        assert sub == case["plan_sub"]
+        plan = (lambda n, w: sub)
+    hj = _CpuJoin(flag=case.get("flag", False), plan=plan)
     ph = {}
+    if case.get("flag"):
+        # a count flagged by bit 63 is an error on every probe path, never a
+        # (negative) row count
+        import pytest as _pt
+        with _pt.raises(RuntimeError, match="overflow"):
+            distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
+                             replicate_max_rows=case.get("replicate", 0), route_bits=case.get("route_bits"),
+                             s_parts=case.get("s_parts"))
+        np.savez(os.path.join(outdir, f"dj{rank}.npz"), r=np.zeros(0, np.int64), s=np.zeros(0, np.int64),
+                 nr=np.array([0]), ns=np.array([0]), mode=np.array([False]))
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     o_r, o_s = distributed_join(hj, rk, rp, sk, sp, capacity=case.get("capacity"), phases=ph,
                                 replicate_max_rows=case.get("replicate", 0), max_rows=case.get("max_rows"),
                                 n_build_global=case["NR"] if case.get("known_nr") else None,
@@ -211,7 +240,8 @@ def _dj_worker(rank, world, port, case, outdir):
                 assert (np.asarray(own) == rank).all()
             else:
                 assert (_np_partition_of(full_sk[o_s.numpy()], world) == rank).all()
-        assert ph.get("folded", False) == (case.get("route_bits", 0) > 0 and (world & (world - 1)) == 0)
+        folded = (case.get("route_bits") or case.get("plan_sub", 0)) > 0 and (world & (world - 1)) == 0
+        assert ph.get("folded", False) == folded
     else:
         assert hj.calls["partition"] == 0 and nrows[0] == case["NR"]
     assert ph["start"].elapsed_time(ph["probed"]) >= 0.0
@@ -242,10 +272,14 @@ def _dj_worker(rank, world, port, case, outdir):
     dict(dist="uniform", NR=2000, NS=2600, hi=300, seed=37, route_bits=2, s_parts=3, world=4, max_rows=101),
     dict(dist="pkfk", NR=4000, NS=6001, frac=0.9, seed=38, route_bits=4, world=3),      # 3 ranks: not folded
     dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=39, route_bits=5, world=1, s_parts=2, capacity=900),
+    # the N = 8 product layout: 8 owners x 2^6 bins (9 routing bits, hj_route_plan's maximum), S in 2 parts
+    dict(dist="pkfk", NR=6000, NS=9001, frac=0.9, seed=40, route_bits=6, world=8),
+    dict(dist="uniform", NR=4000, NS=5000, hi=700, seed=41, plan_n=1 << 28, plan_sub=6, world=8, s_parts=3,
+         max_rows=173),
 ], ids=["pkfk", "dups", "int64_min", "resize_3ranks", "pieces", "replicate", "replicate_dups_3ranks",
         "tiny_4ranks", "known_build_size", "known_build_size_replicate", "s_parts3", "s_parts_overflow",
         "s_parts_empty", "one_rank", "one_rank_s_parts2", "folded", "folded_4ranks_parts", "folded_3ranks_falls_back",
-        "folded_one_rank_parts"])
+        "folded_one_rank_parts", "folded_8ranks_sub6", "folded_8ranks_product_plan_dups"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
     mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
@@ -257,3 +291,31 @@ def test_distributed_join_gloo(case, tmp_path, oracle):
     rk, rp, sk, sp = (np.concatenate([p[i] for p in parts]) for i in range(4))
     er, es = oracle.nested_loop_i64(rk, rp, sk, sp)
     assert oracle.same_multiset(np.concatenate(rs), np.concatenate(ss), er, es)
+
+
+@pytest.mark.parametrize("case", [
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=50, flag=True),                  # shuffle, one part
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=51, flag=True, s_parts=2),       # shuffle, parts
+    dict(dist="pkfk", NR=3000, NS=5000, frac=0.8, seed=52, flag=True, route_bits=3),    # folded
+    dict(dist="pkfk", NR=700, NS=900, frac=1.0, seed=53, flag=True, replicate=1 << 21),  # replicate
+], ids=["shuffle", "shuffle_parts", "folded", "replicate"])
+def test_distributed_join_flagged_count_raises(case, tmp_path):
+    """a probe count with bit 63 set (an internal work list
+    overflowed) must raise on every distributed path instead of reading as a
+    negative M (a silently truncated or empty result)."""
+    mp.spawn(_dj_worker, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
+
+
+def test_checked_count_helpers():
+    """_probe_all / _probe_parts reject a flagged count (no process group)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mlir-hashjoin_amd"))
+    from hashjoin.dist import _probe_all, _probe_parts
+    t = torch.zeros((4, 2), dtype=torch.int64)
+    flagged = lambda tt, o_r, o_s: torch.tensor([3 | -(1 << 63)], dtype=torch.int64)
+    with pytest.raises(RuntimeError, match="overflow"):
+        _probe_all(None, t, 8, flagged)
+    with pytest.raises(RuntimeError, match="overflow"):
+        _probe_parts(None, [lambda: t], 8, 4, "cpu", [flagged])
+    ok = lambda tt, o_r, o_s: torch.tensor([2], dtype=torch.int64)
+    o_r, o_s = _probe_all(None, t, 8, ok)
+    assert o_r.numel() == 2 and o_s.numel() == 2

@@ -419,17 +419,15 @@ def test_i32_reference_scale(hj):
     assert torch.unique(o_r.long() * n + o_s.long()).numel() == m
 
 
-# ---------------------------------------------------------------- XCD split
-# Global-table probe with the probe side routed into 8 groups by the top slot
-# bits (one group per XCD).  Forced on at oracle-checkable sizes; the fast
-# path, the general path (duplicates, INT64_MIN keys) on bucketed tiles and
-# the i32 layout must all match the oracle.
+# ---------------------------------------------------------------- global table
+# The global linear-probing table at oracle-checkable sizes: the fast path,
+# the general path (duplicates, INT64_MIN keys) and the i32 layout.  (The
+# XCD-split variant of this probe measured slower and was removed in round 4.)
 @pytest.mark.parametrize("case", ["pkfk", "dups", "nulls", "i32"])
-def test_xcd_split_vs_oracle(oracle, case):
+def test_global_table_vs_oracle(oracle, case):
     hj = HashJoin(0)
     try:
         hj.set_strategy("global")
-        hj.set_xcd_split(True)
         hj.set_timing(True)
         if case == "pkfk":
             rk, rp, sk, sp = oracle.gen_pkfk_i64(5, 100000, 300000, 0.7)
@@ -454,7 +452,5 @@ def test_xcd_split_vs_oracle(oracle, case):
         o_r, o_s = hj.join(*d)
         assert hj.strategy_used == "global"
         assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp)
-        t = hj.last_timing()
-        assert t["probe_partition"] > 0          # the split ran
     finally:
         hj.close()
