@@ -261,16 +261,37 @@ int64_t hj_host_join_ooc_i64(hj_ctx *ctx, const int64_t *rkey, const int64_t *rp
  * count.
  *
  * Count -> probe reuse: the reference's @countRows leaves its table for
- * @probeRelation (join_v1.mlir:110-176).  Here the count call performs the
- * whole join and keeps the pairs on the device; a following call whose
- * inputs are byte-identical (uploaded again and compared on the device, so
- * a caller that changed its buffers in between gets a fresh join) returns
- * them without building or probing again.  hj_host_memo_hits() counts
- * those reuses.
+ * @probeRelation (join_v1.mlir:110-176).  hj_count_* uploads both relations,
+ * BUILDS and COUNTS (no pairs are materialised) and keeps the built table and
+ * the staged probe side.  A following hj_probe_* with inputs of the same
+ * sizes probes that kept table (no upload, no build) when the inputs are
+ * judged unchanged since the count, under the process-wide reuse mode:
+ *   HJ_REUSE_DIGEST (default): a 128-bit content digest of every input
+ *     memref, taken by the count and again by the probe on host threads
+ *     (four multiply-rotate lanes, hj_capi.cpp digest_mem), matches.  The
+ *     digest is NOT cryptographic: inputs crafted to collide with the counted
+ *     ones would be joined as the counted ones.
+ *   HJ_REUSE_EXACT: every input byte equals the count's (the count keeps a
+ *     compacted host copy of its inputs -- host memory of the inputs' size --
+ *     and the probe compares with memcmp on host threads).
+ *   HJ_REUSE_OFF: nothing is kept; every hj_probe_* runs the whole join.
+ * Anything else (changed inputs, another mode, another build in between)
+ * runs the whole join.  Reused or not, the result is the join of the inputs
+ * passed to hj_probe_*.
+ * Output delivery is speculative: while the verdict is computed the kept
+ * table's pairs are already written into the caller's output memrefs (when
+ * their size equals the count's M); if the inputs turn out changed, the fresh
+ * join's pairs are written over them.  On any error return the contents of
+ * the output memrefs are undefined.  hj_host_memo_hits() counts the reuses.
  *
  * Threading: these host-memref entry points (and the ciface / rows /
  * selection ones below) use one default context per device; each call holds
  * that context's lock, so concurrent callers are serialised, never mixed. */
+#define HJ_REUSE_DIGEST 0
+#define HJ_REUSE_EXACT 1
+#define HJ_REUSE_OFF 2
+/* Set the reuse mode; returns the previous one, or HJ_ERR_ARG. */
+int hj_host_set_reuse(int mode);
 int64_t hj_host_memo_hits(void);
 int64_t hj_count_i32(int32_t *r_alloc, int32_t *r_align, int64_t r_off, int64_t r_size, int64_t r_stride,
                      int32_t *s_alloc, int32_t *s_align, int64_t s_off, int64_t s_size, int64_t s_stride);

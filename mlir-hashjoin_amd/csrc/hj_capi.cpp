@@ -12,6 +12,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -124,7 +125,7 @@ struct hj_ctx {
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
-    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, wstart, work_start, work_desc, scan_sums;
+    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, wstart, work_start, work_desc, scan_sums, scan_state;
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
@@ -161,6 +162,9 @@ struct hj_ctx {
         int64_t nr = 0, ns = 0;
         Digest dr, ds;   // R (keys, payloads), S (keys, payloads)
         int64_t m = 0;
+        int reuse = 0;   // HJ_REUSE_* the count ran under
+        // HJ_REUSE_EXACT: the count's inputs, compacted (keys, then payloads)
+        std::vector<unsigned char> cr, cs;
     } memo;
     long long memo_hits = 0;
     // the last radix probe's shape, for hj_ctx_join_kernel (the kernel itself
@@ -288,6 +292,13 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     HJ_TRY(ensure_buf(c->work_start, (size_t)hj::radix_work_words(pl, fin.max_runs) * 4));
     HJ_TRY(ensure_buf(c->work_desc, items * hj::radix_item_desc_bytes()));
     HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
+    {
+        // the one-launch scan's tile words: zero on allocation, and every
+        // scan leaves them zero
+        const size_t had = c->scan_state.bytes;
+        HJ_TRY(ensure_buf(c->scan_state, ((P + 1) / 1024 + 4) * 8));
+        if (c->scan_state.bytes != had) HJ_HIP(hipMemset(c->scan_state.p, 0, c->scan_state.bytes));
+    }
     return HJ_OK;
 }
 
@@ -302,6 +313,7 @@ hj::RadixWork radix_work(hj_ctx *c) {
     w.tdesc = c->tdesc.p;
     w.wstart = (unsigned *)c->wstart.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
+    w.scan_state = (unsigned long long *)c->scan_state.p;
     return w;
 }
 
@@ -368,7 +380,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     if (src.n < 0 || (src.n > 0 && !src.key)) HJ_FAIL(HJ_ERR_ARG, "bad probe relation");
     if (!count_only && (cap < 0 || (cap > 0 && (!out_r || !out_s)))) HJ_FAIL(HJ_ERR_ARG, "bad output");
     HJ_TRY(set_device(c));
-    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+    // (the radix join zeroes the counter in its work-map kernel: no memset launch)
     const bool radix = c->used == HJ_STRATEGY_RADIX || (c->dual && src.n >= kRadixProbeMinRows);
     c->probe_used = radix ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
     c->join_ran = false;
@@ -396,6 +408,7 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         c->rec_mid = c->timing;
         return HJ_OK;
     }
+    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
     hj::OutDev out;
     out.r = out_r;
     out.s = out_s;
@@ -455,6 +468,7 @@ hj::SrcDev src_col32(const int32_t *k, int64_t n, int64_t row_base) {
 
 // ---------------------------------------------------------------- host path
 std::mutex g_default_mu;
+std::atomic<int> g_reuse{HJ_REUSE_DIGEST};   // hj_host_set_reuse
 std::map<int, hj_ctx *> g_default;
 
 hj_ctx *default_ctx() {
@@ -645,6 +659,46 @@ Digest digest_mem(const void *aligned, int64_t off, int64_t size, int64_t stride
     return d;
 }
 
+// ---- exact copies (HJ_REUSE_EXACT): the count keeps the inputs' bytes,
+// compacted; the probe compares its memrefs with them (same threading as
+// digest_mem: up to 8 host threads, >= 4 MiB each).
+template <class F>
+void chunked(int64_t size, int esz, F &&work) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    unsigned T = (unsigned)((size * esz) >> 22) + 1;
+    if (T > 8) T = 8;
+    if (hw && T > hw) T = hw;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; ++t) th.emplace_back(work, size * t / T, size * (t + 1) / T);
+    work((int64_t)0, size / T);
+    for (auto &x : th) x.join();
+}
+
+void gather_mem(const void *aligned, int64_t off, int64_t size, int64_t stride, int esz, unsigned char *dst) {
+    if (size <= 0 || !aligned) return;
+    const char *base = (const char *)aligned + off * esz;
+    chunked(size, esz, [&](int64_t e0, int64_t e1) {
+        if (stride == 1) std::memcpy(dst + e0 * esz, base + e0 * esz, (size_t)(e1 - e0) * (size_t)esz);
+        else
+            for (int64_t e = e0; e < e1; ++e) std::memcpy(dst + e * esz, base + e * stride * esz, (size_t)esz);
+    });
+}
+
+bool same_mem(const void *aligned, int64_t off, int64_t size, int64_t stride, int esz, const unsigned char *ref) {
+    if (size <= 0) return true;
+    if (!aligned) return false;
+    const char *base = (const char *)aligned + off * esz;
+    std::atomic<bool> diff{false};
+    chunked(size, esz, [&](int64_t e0, int64_t e1) {
+        bool d = false;
+        if (stride == 1) d = std::memcmp(ref + e0 * esz, base + e0 * esz, (size_t)(e1 - e0) * (size_t)esz) != 0;
+        else
+            for (int64_t e = e0; e < e1 && !d; ++e) d = std::memcmp(ref + e * esz, base + e * stride * esz, (size_t)esz) != 0;
+        if (d) diff = true;
+    });
+    return !diff;
+}
+
 // One host relation of the memref ABI: a key column and (int64 rows) an
 // optional payload column (null: payload = row id, the reference's rowId,
 // join_v1.mlir:255).
@@ -655,6 +709,20 @@ struct HostRel {
     int64_t p_off, p_stride;
     int64_t n;
 };
+
+void copy_rel(const HostRel &r, int esz, std::vector<unsigned char> &out) {
+    const size_t col = (size_t)(r.n > 0 ? r.n : 0) * (size_t)esz;
+    out.resize(col * (r.p ? 2 : 1));
+    gather_mem(r.k, r.k_off, r.n, r.k_stride, esz, out.data());
+    if (r.p) gather_mem(r.p, r.p_off, r.n, r.p_stride, esz, out.data() + col);
+}
+
+bool same_rel(const HostRel &r, int esz, const std::vector<unsigned char> &ref) {
+    const size_t col = (size_t)(r.n > 0 ? r.n : 0) * (size_t)esz;
+    if (ref.size() != col * (r.p ? 2 : 1)) return false;
+    return same_mem(r.k, r.k_off, r.n, r.k_stride, esz, ref.data()) &&
+           (!r.p || same_mem(r.p, r.p_off, r.n, r.p_stride, esz, ref.data() + col));
+}
 
 Digest digest_rel(const HostRel &r, int esz) {
     Digest d = digest_mem(r.k, r.k_off, r.n, r.k_stride, esz);
@@ -739,16 +807,24 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     hipStream_t st = c->host_stream;
     const int esz = layout == kWide ? 8 : 4;
     hj_ctx::Memo &mm = c->memo;
+    const int reuse = g_reuse.load();
     Digest dr, ds;
+    bool same_r = false, same_s = false;   // HJ_REUSE_EXACT: byte-equal to the count's inputs
     if (delivered) *delivered = false;
-    if (mode == kHostProbe && mm.valid && mm.layout == layout && mm.nr == r.n && mm.ns == s.n) {
+    if (mode == kHostProbe && mm.valid && mm.reuse == reuse && reuse != HJ_REUSE_OFF && mm.layout == layout &&
+        mm.nr == r.n && mm.ns == s.n) {
         int rc = HJ_OK;
         int64_t mp = 0;
         bool sent = false;
         {
             Joiner dig_r, dig_s;
-            dig_r.t = std::thread([&] { dr = digest_rel(r, esz); });
-            dig_s.t = std::thread([&] { ds = digest_rel(s, esz); });
+            if (reuse == HJ_REUSE_EXACT) {
+                dig_r.t = std::thread([&] { same_r = same_rel(r, esz, mm.cr); });
+                dig_s.t = std::thread([&] { same_s = same_rel(s, esz, mm.cs); });
+            } else {
+                dig_r.t = std::thread([&] { dr = digest_rel(r, esz); });
+                dig_s.t = std::thread([&] { ds = digest_rel(s, esz); });
+            }
             const hj::SrcDev src = layout == kWide
                                        ? src_cols64((const int64_t *)c->dbuf[7], (const int64_t *)c->dbuf[7] + s.n, s.n)
                                        : src_col32((const int32_t *)c->dbuf[7], s.n, 0);
@@ -760,7 +836,7 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
             }
         }
         if (rc != HJ_OK) return rc;
-        if (dr == mm.dr && ds == mm.ds) {
+        if (reuse == HJ_REUSE_EXACT ? (same_r && same_s) : (dr == mm.dr && ds == mm.ds)) {
             ++c->memo_hits;
             *m = mp;
             *d_or = c->dbuf[2];
@@ -778,9 +854,15 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     hj::SrcDev rsrc, ssrc;
     {
         Joiner dig;
-        if (mode == kHostCount) dig.t = std::thread([&] {   // overlapped with the upload
+        mm.cr.clear();
+        mm.cs.clear();
+        if (mode == kHostCount && reuse == HJ_REUSE_DIGEST) dig.t = std::thread([&] {   // overlapped with the upload
             dr = digest_rel(r, esz);
             ds = digest_rel(s, esz);
+        });
+        else if (mode == kHostCount && reuse == HJ_REUSE_EXACT) dig.t = std::thread([&] {
+            copy_rel(r, esz, mm.cr);
+            copy_rel(s, esz, mm.cs);
         });
         HJ_TRY(upload_rel(c, layout, r, dr_buf, &rsrc));
         HJ_TRY(upload_rel(c, layout, s, ds_buf, &ssrc));
@@ -796,13 +878,16 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     HJ_TRY(do_probe(c, layout, ssrc, nullptr, nullptr, 0, (uint64_t *)c->dcount, true, st));
     HJ_HIP(hipMemcpyAsync(&cnt, c->dcount, 8, hipMemcpyDeviceToHost, st));
     HJ_HIP(hipStreamSynchronize(st));
+    // (a flagged count is an error, never a row count -- and never memoised)
+    if (cnt >> 63) HJ_FAIL(HJ_ERR_CAPACITY, "count: internal work list overflow (count flagged)");
     mm.layout = layout;
     mm.nr = r.n;
     mm.ns = s.n;
     mm.dr = dr;
     mm.ds = ds;
     mm.m = (int64_t)cnt;
-    mm.valid = true;
+    mm.reuse = reuse;
+    mm.valid = reuse != HJ_REUSE_OFF;
     *m = (int64_t)cnt;
     *d_or = *d_os = nullptr;
     return HJ_OK;
@@ -934,6 +1019,11 @@ int hj_device_info(int device, int64_t out[8]) {
     return HJ_OK;
 }
 
+int hj_host_set_reuse(int mode) {
+    if (mode != HJ_REUSE_DIGEST && mode != HJ_REUSE_EXACT && mode != HJ_REUSE_OFF) HJ_FAIL(HJ_ERR_ARG, "bad reuse mode");
+    return g_reuse.exchange(mode);
+}
+
 int64_t hj_host_memo_hits(void) {
     hj_ctx *c = default_ctx();
     if (!c) return HJ_ERR_HIP;
@@ -974,7 +1064,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->runs, &sb->rstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums,
+    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums, &c->scan_state,
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
                    &c->route_hist, &c->route_sums})
         free_buf(*b);
@@ -1264,8 +1354,7 @@ int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
         HJ_FAIL(HJ_ERR_ARG, "bad routed layout");
     hipStream_t st = (hipStream_t)stream;
     HJ_TRY(set_device(c));
-    HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
-    c->probe_used = HJ_STRATEGY_RADIX;
+    c->probe_used = HJ_STRATEGY_RADIX;   // (radix_join zeroes d_count)
     HJ_TRY(ensure_radix_scratch(c, c->sset, n, 16, c->plan));
     record(c, kEvProbe0, st);
     HJ_HIP(hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, nbins, c->plan,

@@ -161,6 +161,7 @@ struct RadixWork {                 // scratch shared by the partition passes
     void *tdesc;                   // >= radix_tiles(n, P) * 16 B: bucketed-pass tile descriptors
     unsigned *wstart;              // >= 1025: per-workgroup bucket id ranges of a pass
     unsigned long long *scan_sums; // >= P / 8192 + 2
+    unsigned long long *scan_state;// >= P / 1024 + 4, zero between calls (the one-launch scan's tile words)
 };
 
 struct RadixNeed {                 // sizes of one bucket set

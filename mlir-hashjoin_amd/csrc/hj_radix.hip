@@ -46,6 +46,11 @@ constexpr int kTile = 4096;        // rows per partition-pass tile (LDS staging:
 constexpr int kPassThreads = 1024; // one workgroup per CU
 constexpr int kPassRows = kTile / kPassThreads;
 constexpr int kMaxFan = 512;       // bins per pass (9 bits)
+// passes of <= 8 bits: half-size workgroups (512 threads, 2048-row tiles,
+// 256 bins' line tails: ~70 KiB of LDS), two per CU, so one workgroup's LDS
+// phases overlap the other's loads and stores
+constexpr int kSmallPassThreads = 512;
+constexpr int kSmallFan = 256;
 constexpr int kJoinItems = 5;      // S rows per thread per sub-chunk of the join kernel (2560 rows = 10 buckets)
 constexpr int kJoinSub = 8;        // sub-chunks per work item (one table build serves all)
 constexpr int kPackedRow = 3;      // SrcForm of packed-row inputs
@@ -82,7 +87,10 @@ struct Row<false> {   // i32 key (zero-extended) / i32 row id, packed key << 32 
 
 // Streaming (non-temporal) loads/stores for data touched once per kernel.
 // Measured (profiles/r01_nt_variants.txt): join loads + stores nt -2.7 %;
-// pass stores nt +66 % (they defeat the L2's line assembly), pass loads nt +3 %.
+// pass loads nt +3 %.  Pass stores: nt cost +66 % while a line's old tail
+// and new rows went out in two store instructions (nt bypasses the L2 that
+// assembled them); since round 4 every line is one instruction's (k_pass's
+// line stores) and nt stores are 0.3-2.6 % faster (profiles/r04_line_stores.txt).
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 template <bool NT, typename T>
 __device__ __forceinline__ T ld_s(const T *p) {
@@ -111,7 +119,7 @@ __device__ __forceinline__ void st_s(T *p, const T &v) {
         __builtin_nontemporal_store(v, p);
     }
 }
-constexpr bool kNtPassLd = false, kNtPassSt = false;
+constexpr bool kNtPassLd = false, kNtPassSt = true;
 constexpr bool kNtJoinLd = true, kNtJoinSt = true;
 
 // Row `row` of a pass input in form FORM.
@@ -218,6 +226,115 @@ __global__ __launch_bounds__(1024) void k_scan_add(u64 *a, u64 n, const u64 *sum
         if (base + i < n) a[base + i] += add;
 }
 
+__device__ __forceinline__ unsigned runs_of(unsigned fill) { return (fill + (1u << kRunLog) - 1) >> kRunLog; }
+
+// --------------------------------------------------------------- one-launch scan
+// Exclusive scan in ONE launch (decoupled look-back) for the listings of the
+// radix passes and the join's work map: tiles of kScanBlock elements are
+// taken in ticket order; a tile publishes its aggregate, wave 0 looks back
+// over its predecessors' words (aggregate, or inclusive prefix: stop there),
+// then the tile publishes its inclusive prefix.  A word is flag << 62 |
+// value; both sides use 8-B device-scope atomic RMWs (executed coherently
+// across the XCDs' L2s).  Forward progress: a tile only waits on tiles
+// whose tickets were drawn earlier, i.e. by running workgroups.
+// state: one word per tile + ticket + done counter, zero on entry; the last
+// workgroup to finish clears them for the next call (a kernel boundary
+// orders that before any later launch).
+constexpr u64 kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 62) - 1;
+// tiles of 1024 elements (256 threads x 4): 2^17 partitions spread over 129
+// workgroups instead of 17 (the scan is latency-bound, not byte-bound)
+constexpr int kLbThreads = 256, kLbPer = 4, kLbTile = kLbThreads * kLbPer;
+
+// MAP (the join's work map, chunk_map's three launches in one): element p <
+// nseg is the chunk count of segment p -- ceil(len_a(p) / chunk), 0 when
+// off_b says segment p of b is empty -- and, with split, its heavy count
+// (the count when >= 2) in bits 31..61; element nseg is 0.  The scan goes
+// to scan[] as heavy << 32 | count (k_item_desc's split order), its low half
+// to start[], and owner[w] = p for segment p's chunks.
+struct ChunkMapArgs {
+    const u64 *off_a, *off_b;
+    unsigned chunk;
+    bool split;
+    unsigned *start, *owner;
+};
+
+template <bool MAP>
+__global__ __launch_bounds__(kLbThreads) void k_scan_lb(u64 *a, u64 n, u64 *state, ChunkMapArgs mp) {
+    __shared__ u64 wsum[16];
+    __shared__ u64 s_pre;
+    __shared__ unsigned s_tile;
+    const unsigned nt = (unsigned)((n + kLbTile - 1) / kLbTile);
+    if (threadIdx.x == 0) s_tile = (unsigned)atomicAdd(&state[nt], 1ull);
+    __syncthreads();
+    const unsigned t = s_tile;
+    const u64 base = (u64)t * kLbTile + (u64)threadIdx.x * kLbPer;
+    u64 v[kLbPer], s = 0;
+#pragma unroll
+    for (int i = 0; i < kLbPer; ++i) {
+        const u64 e = base + i;
+        if constexpr (MAP) {
+            v[i] = 0ull;
+            if (e + 1 < n) {   // (element n - 1 = nseg: 0)
+                const u64 len = mp.off_a[e + 1] - mp.off_a[e];
+                const bool live = mp.off_b ? (mp.off_b[e + 1] > mp.off_b[e]) : true;
+                const u64 c = live ? (len + mp.chunk - 1) / mp.chunk : 0ull;
+                v[i] = mp.split && c >= 2 ? c | (c << 31) : c;
+            }
+        } else {
+            v[i] = e < n ? a[e] : 0ull;
+        }
+        s += v[i];
+    }
+    u64 total;
+    u64 run = block_excl_scan<kLbThreads>(s, wsum, &total);
+    if (threadIdx.x < 64) {
+        const unsigned lane = threadIdx.x;
+        u64 pre = 0;
+        if (t == 0) {
+            if (lane == 0) atomicExch(&state[0], kLbInc | total);
+        } else {
+            if (lane == 0) atomicExch(&state[t], kLbAgg | total);
+            // wave 0 reads 64 predecessors at a time (lane j: tile w - 1 - j)
+            for (unsigned w = t; w > 0;) {
+                const u64 x = lane < w ? atomicOr(&state[w - 1 - lane], 0ull) : kLbInc;   // (past tile 0: a stop)
+                const u64 inc = __ballot((x >> 62) == 2ull), none = __ballot((x >> 62) == 0ull);
+                const u64 upto = inc ? (inc & (~inc + 1ull)) * 2ull - 1ull : ~0ull;   // lanes up to the nearest stop
+                if (none & upto) {   // a predecessor has not published yet: read again
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                pre += wave_incl_add64((upto >> lane) & 1ull && lane < w ? (x & kLbVal) : 0ull);
+                pre = __shfl(pre, 63);
+                if (inc) break;
+                w = w > 64u ? w - 64u : 0u;
+            }
+            if (lane == 0) atomicExch(&state[t], kLbInc | (pre + total));
+        }
+        if (lane == 0) s_pre = pre;
+    }
+    __syncthreads();
+    run += s_pre;
+#pragma unroll
+    for (int i = 0; i < kLbPer; ++i) {
+        const u64 e = base + i;
+        if (e < n) {
+            if constexpr (MAP) {
+                const unsigned lo = (unsigned)(run & 0x7FFFFFFFull);
+                a[e] = ((run >> 31) << 32) | lo;
+                mp.start[e] = lo;
+                const unsigned c = (unsigned)(v[i] & 0x7FFFFFFFull);
+                for (unsigned k = 0; k < c; ++k) mp.owner[lo + k] = (unsigned)e;
+            } else {
+                a[e] = run;
+            }
+        }
+        run += v[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(&state[nt + 1], 1ull) == (u64)nt - 1ull)
+        for (unsigned k = 0; k < nt + 2; ++k) atomicExch(&state[k], 0ull);
+}
+
 // --------------------------------------------------------------- partition pass
 struct PassArgs {
     SrcDev in;                   // pass-1 source (FORM != kBucketed)
@@ -241,16 +358,17 @@ struct PassArgs {
     int shift;                   // bin = (hash >> shift) & (F - 1)
     int fbits;
     u64 *prof = nullptr;         // diagnostics (ABL & 8): per workgroup, cycles per phase
-    // zeroed by the pass for the listing that follows it (its per-partition
-    // run counts and cursors): two memsets and a copy fewer per pass
-    u64 *zero_a = nullptr, *zero_b = nullptr;
-    u64 zero_n = 0;
+    // the listing's per-partition run counts (zeroed by the plan kernel that
+    // runs before the pass): a bucket adds its runs when it is full or closed
+    // (k_bcount's count, done where the buckets are made); null: no listing
+    u64 *rcnt = nullptr;
     // EXACT passes (the folded routing): workgroup w writes bin b's rows to
     // out rows [slot_base[b * G + w], ...) -- exact, contiguous per bin, no
     // buckets; out_max_rows bounds every write
     const u64 *slot_base = nullptr;
     u64 out_max_rows = 0;
     int hash_top = 0;   // EXACT: bin = the top fbits of the hash (shift = 64 - fbits)
+    unsigned tile_rows = kTile;   // rows per tile of this pass's kernel variant (its threads x kPassRows)
 };
 
 // A bucketed pass's tile: runs [lo, lo + cnt) (cnt <= kTile / 64) of segment seg.
@@ -260,23 +378,24 @@ struct TileDesc {
 };
 
 __global__ __launch_bounds__(256) void k_tile_desc(const unsigned *tile_start, const unsigned *tile_owner,
-                                                   const u64 *rstart, int nseg, unsigned bound, TileDesc *desc) {
+                                                   const u64 *rstart, int nseg, unsigned bound, TileDesc *desc,
+                                                   unsigned rpt) {
     const unsigned t = blockIdx.x * 256 + threadIdx.x;
     if (t >= tile_start[nseg] || t >= bound) return;
     const unsigned seg = tile_owner[t];
-    const u64 lo = rstart[seg] + (u64)(t - tile_start[seg]) * (unsigned)(kTile >> kRunLog);
+    const u64 lo = rstart[seg] + (u64)(t - tile_start[seg]) * rpt;
     const u64 e = rstart[seg + 1];
     TileDesc d;
     d.lo = lo;
-    d.cnt = (unsigned)(e - lo < (u64)(kTile >> kRunLog) ? e - lo : (u64)(kTile >> kRunLog));
+    d.cnt = (unsigned)(e - lo < (u64)rpt ? e - lo : (u64)rpt);
     d.seg = seg;
     desc[t] = d;
 }
 
-template <int FORM>
+template <int FORM, int TILE = kTile>
 __device__ __forceinline__ unsigned pass_tiles(const PassArgs &a) {
     if constexpr (FORM == kBucketed) return a.tile_start[a.nseg];
-    else return (unsigned)((a.n + kTile - 1) / kTile);
+    else return (unsigned)((a.n + TILE - 1) / TILE);
 }
 
 // Row v (0 <= v < kTile) of the row-source tile starting at row lo; false
@@ -312,21 +431,27 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, u64 lo, unsigned v, 
 // give the bases): rows land grouped by bin with no holes, so a bin's rows
 // can be sent as one message.  A slot's first line is shared with the slot
 // before it (written partly, once); every other line is written whole.
-template <bool WIDE, int FORM, int ABL = 0, bool EXACT = false>
-__global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
+template <bool WIDE, int FORM, int ABL = 0, bool EXACT = false, int NT = kPassThreads, int FMAX = kMaxFan>
+__global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
-    for (u64 i = (u64)blockIdx.x * kPassThreads + threadIdx.x; i < a.zero_n; i += (u64)gridDim.x * kPassThreads) {
-        a.zero_a[i] = 0ull;
-        a.zero_b[i] = 0ull;
-    }
     constexpr int IT = kPassRows;
+    constexpr int kTile = NT * IT;          // (shadows the file's: this variant's tile)
+    constexpr int kPassThreads = NT;
+    constexpr int kMaxFan = FMAX;
+    static_assert(FMAX == 256 || FMAX == 512, "wave 0 scans 4 or 8 bins per lane");
     constexpr unsigned L = 128 / sizeof(T);   // rows per line
     __shared__ T stage[kTile];
     __shared__ T tail[kMaxFan * (L - 1)];   // bin b: rows of positions [fill & ~(L-1), fill)
-    __shared__ unsigned short sb[kTile];
     __shared__ __attribute__((aligned(16))) unsigned cnt[kMaxFan], start[kMaxFan], cur[kMaxFan], fill[kMaxFan],
-        nbase[kMaxFan];
+        nbase[kMaxFan], lstart[kMaxFan];
+    // the tile's complete lines, bin by bin: line x of the tile is a line of
+    // bin lbin[x] (its (x - lstart[b])-th), written by L lanes of ONE store
+    // instruction (old tail rows + new rows), so no line is ever stored in
+    // two parts
+    constexpr int kLines = (kTile + kMaxFan * (L - 1)) / L;
+    __shared__ unsigned short lbin[kLines];
+    __shared__ unsigned s_nl;
     // EXACT: out row of bin b's position 0 (the slot base rounded down to a
     // line; positions below cur[b] belong to the slot before)
     __shared__ u64 cbase[EXACT ? kMaxFan : 1];
@@ -341,7 +466,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     __shared__ unsigned s_hole;
     const unsigned F = 1u << a.fbits;
     const unsigned PB = 1u << a.out_pbl;
-    const unsigned T_ = pass_tiles<FORM>(a);
+    const unsigned T_ = pass_tiles<FORM, kTile>(a);
     const unsigned t0 = (unsigned)((u64)blockIdx.x * T_ / gridDim.x);
     const unsigned t1 = (unsigned)((u64)(blockIdx.x + 1) * T_ / gridDim.x);
     T *out = (T *)a.out_rows;
@@ -396,6 +521,7 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             if (cur[b] != kNoBucket && cur[b] < a.max_buckets) {
                 for (unsigned i = 0; i < tl; ++i) out[((u64)cur[b] << a.out_pbl) + (f - tl + i)] = tail[b * (L - 1) + i];
                 a.bfill[cur[b]] = f;
+                if (a.rcnt) atomicAdd(&a.rcnt[((unsigned)seg_cur << a.fbits) | b], (u64)runs_of(f));
             }
             cur[b] = kNoBucket;
             fill[b] = PB;
@@ -575,49 +701,60 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             // fresh buckets each bin needs (-> nbase, relative); the tile's
             // fresh buckets are the next ids of the workgroup's range
             const int lane = threadIdx.x;
-            // (8 bins per lane moved as two 16-B LDS accesses per array:
-            // wave 0 alone is on the critical path here)
-            unsigned c[8], k[8], s = 0, sk = 0;
-            {
-                const uint4 c0 = ((const uint4 *)cnt)[lane * 2], c1 = ((const uint4 *)cnt)[lane * 2 + 1];
-                const uint4 f0 = ((const uint4 *)fill)[lane * 2], f1 = ((const uint4 *)fill)[lane * 2 + 1];
-                const unsigned cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-                const unsigned fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            // (BPL bins per lane moved as 16-B LDS accesses per array: wave
+            // 0 alone is on the critical path here)
+            constexpr int BPL = FMAX / 64, Q = BPL / 4;
+            unsigned c[BPL], k[BPL], ln[BPL], s = 0, sk = 0, sl = 0;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    c[j] = lane * 8 + j < F ? cv[j] : 0u;
-                    k[j] = (!EXACT && c[j]) ? (fv[j] + c[j] - 1) >> a.out_pbl : 0u;
+            for (int qd = 0; qd < Q; ++qd) {
+                const uint4 c4 = ((const uint4 *)cnt)[lane * Q + qd];
+                const uint4 f4 = ((const uint4 *)fill)[lane * Q + qd];
+                const unsigned cv[4] = {c4.x, c4.y, c4.z, c4.w};
+                const unsigned fv[4] = {f4.x, f4.y, f4.z, f4.w};
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int j = qd * 4 + jj;
+                    c[j] = (unsigned)(lane * BPL + j) < F ? cv[jj] : 0u;
+                    k[j] = (!EXACT && c[j]) ? (fv[jj] + c[j] - 1) >> a.out_pbl : 0u;
+                    // complete lines: the old tail's and the new rows'
+                    ln[j] = c[j] ? ((fv[jj] & (L - 1)) + c[j]) / L : 0u;
                     s += c[j];
                     sk += k[j];
+                    sl += ln[j];
                 }
             }
             {   // the largest bin (count << 16 | bin), for the next tile's count
                 unsigned mx = 0u;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const unsigned y = (c[j] << 16) | (lane * 8u + j);
+                for (int j = 0; j < BPL; ++j) {
+                    const unsigned y = (c[j] << 16) | (unsigned)(lane * BPL + j);
                     mx = y > mx ? y : mx;
                 }
                 mx = wave_max_all(mx);
                 if (lane == 0) s_hot = (mx >> 16) > (unsigned)(kTile / 8) ? (mx & 0xffffu) : 0xFFFFFFFFu;
             }
-            const unsigned x = wave_incl_add(s), xk = wave_incl_add(sk);
-            unsigned run = x - s, runk = xk - sk;
-            unsigned sv[8], nv[8];
+            const unsigned x = wave_incl_add(s), xk = wave_incl_add(sk), xl = wave_incl_add(sl);
+            unsigned run = x - s, runk = xk - sk, runl = xl - sl;
+            unsigned sv[BPL], nv[BPL], lv[BPL];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < BPL; ++j) {
                 sv[j] = run;
                 nv[j] = runk;
+                lv[j] = runl;
                 run += c[j];
                 runk += k[j];
+                runl += ln[j];
             }
-            if (lane * 8 < F) {   // (entries of bins >= F are written but never read)
-                ((uint4 *)start)[lane * 2] = make_uint4(sv[0], sv[1], sv[2], sv[3]);
-                ((uint4 *)start)[lane * 2 + 1] = make_uint4(sv[4], sv[5], sv[6], sv[7]);
-                ((uint4 *)nbase)[lane * 2] = make_uint4(nv[0], nv[1], nv[2], nv[3]);
-                ((uint4 *)nbase)[lane * 2 + 1] = make_uint4(nv[4], nv[5], nv[6], nv[7]);
+            if ((unsigned)(lane * BPL) < F) {   // (entries of bins >= F are written but never read)
+#pragma unroll
+                for (int qd = 0; qd < Q; ++qd) {
+                    ((uint4 *)start)[lane * Q + qd] = make_uint4(sv[qd * 4], sv[qd * 4 + 1], sv[qd * 4 + 2], sv[qd * 4 + 3]);
+                    ((uint4 *)nbase)[lane * Q + qd] = make_uint4(nv[qd * 4], nv[qd * 4 + 1], nv[qd * 4 + 2], nv[qd * 4 + 3]);
+                    ((uint4 *)lstart)[lane * Q + qd] = make_uint4(lv[qd * 4], lv[qd * 4 + 1], lv[qd * 4 + 2], lv[qd * 4 + 3]);
+                }
             }
             if (lane == 63) {
+                s_nl = xl;
                 s_nb = id_next;
                 s_nend = id_end;
                 id_next = xk < id_end - id_next ? id_next + xk : id_end;
@@ -625,51 +762,53 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(1);
+        // Bin b's rows now span positions [fill, fill + cnt) of its bucket
+        // run; lines end below E = (fill + cnt) & ~(L - 1).  Rows below E go
+        // to the stage (packed by bin), the rest become the bin's new tail
+        // (kept in registers until the old tails have been read).
+        unsigned tpos[IT];   // new tail index of row i, or ~0
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
+            tpos[i] = 0xFFFFFFFFu;
             if (br[i] == 0xFFFFFFFFu) continue;
-            const unsigned b = br[i] >> 16;
-            const unsigned pos = start[b] + (br[i] & 0xffffu);
-            stage[pos] = row[i];
-            sb[pos] = (unsigned short)b;
+            const unsigned b = br[i] >> 16, rk = br[i] & 0xffffu;
+            const unsigned f = fill[b], p = f + rk, e = (f + cnt[b]) & ~(L - 1);
+            if (p >= e) tpos[i] = b * (L - 1) + (p - e);
+            else stage[start[b] + rk] = row[i];
+        }
+        // the line -> bin map (a bin owner per thread)
+        for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
+            const unsigned c = cnt[b];
+            if (!c) continue;
+            const unsigned nl = ((fill[b] & (L - 1)) + c) / L, l0 = lstart[b];
+            for (unsigned x = 0; x < nl; ++x) lbin[l0 + x] = (unsigned short)b;
         }
         __syncthreads();
         mark(2);
-        // Bin b's rows now span positions [fill, fill + cnt) of its bucket
-        // run; lines end below E = (fill + cnt) & ~(L - 1).  Rows below E
-        // are stored (the tail's first), the rest become the new tail.
-        const unsigned tn = start[F - 1] + cnt[F - 1];
-        unsigned tpos[IT];   // new tail index of staged row j, or ~0
-#pragma unroll
-        for (int i = 0; i < IT; ++i) {
-            const unsigned j = (unsigned)i * kPassThreads + threadIdx.x;
-            tpos[i] = 0xFFFFFFFFu;
-            if (j >= tn) continue;
-            const unsigned b = sb[j];
-            const unsigned f = fill[b];
-            const unsigned p = f + (j - start[b]), e = (f + cnt[b]) & ~(L - 1);
-            if (p >= e) {
-                tpos[i] = b * (L - 1) + (p - e);
-                continue;
+        {
+            // complete lines: L lanes per line, 64 / L lines per store
+            // instruction; a line's rows are the bin's old tail rows, then
+            // its staged new rows
+            constexpr unsigned LPW = 64u / L;
+            const unsigned nl = s_nl, g = (threadIdx.x & 63u) / L, r = threadIdx.x & (L - 1);
+            for (unsigned l0 = wave * LPW; l0 < nl; l0 += (unsigned)(kPassThreads / 64) * LPW) {
+                const unsigned x = l0 + g;
+                if (x >= nl) continue;
+                const unsigned b = lbin[x];
+                const unsigned f = fill[b], tl0 = f & (L - 1);
+                const unsigned off = (x - lstart[b]) * L + r;
+                const unsigned p = f - tl0 + off;
+                if (EXACT && p < cur[b]) continue;   // (the slot before's rows)
+                const T v = off < tl0 ? tail[b * (L - 1) + off] : stage[start[b] + (off - tl0)];
+                const u64 o = slot(b, p);
+                if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, v);
             }
-            const u64 o = slot(b, p);
-            if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, stage[j]);
-        }
-        for (unsigned q = threadIdx.x; q < F * (L - 1); q += kPassThreads) {
-            const unsigned b = q / (L - 1), i = q - b * (L - 1);
-            const unsigned f = fill[b], tl0 = f & (L - 1);
-            if (i >= tl0) continue;
-            const unsigned p = f - tl0 + i;
-            if (p >= ((f + cnt[b]) & ~(L - 1))) continue;   // line still incomplete: stays
-            if (EXACT && p < cur[b]) continue;                 // (the slot before's rows)
-            const u64 o = slot(b, p);
-            if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>(out + o, tail[q]);
         }
         __syncthreads();
         mark(3);
 #pragma unroll
         for (int i = 0; i < IT; ++i)
-            if (tpos[i] != 0xFFFFFFFFu) tail[tpos[i]] = stage[(unsigned)i * kPassThreads + threadIdx.x];
+            if (tpos[i] != 0xFFFFFFFFu) tail[tpos[i]] = row[i];
         for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
             const unsigned c = cnt[b];
             cnt[b] = 0u;
@@ -682,15 +821,23 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
             const unsigned k = (f + c - 1) >> a.out_pbl;
             if (k) {
                 // the replaced open bucket is full (all its lines stored);
-                // record the fresh ones
-                if (cur[b] != kNoBucket && cur[b] < a.max_buckets) a.bfill[cur[b]] = PB;
+                // record the fresh ones, and the full ones' runs for the listing
+                unsigned full = 0;
+                if (cur[b] != kNoBucket && cur[b] < a.max_buckets) {
+                    a.bfill[cur[b]] = PB;
+                    ++full;
+                }
                 const unsigned pid = ((unsigned)seg << a.fbits) | b;
                 for (unsigned i = 0; i < k; ++i) {
                     const unsigned bk = fresh(nbase[b] + i);
                     if (bk == kNoBucket) continue;
                     a.bbin[bk] = pid;
-                    if (i + 1 < k) a.bfill[bk] = PB;
+                    if (i + 1 < k) {
+                        a.bfill[bk] = PB;
+                        ++full;
+                    }
                 }
+                if (a.rcnt && full) atomicAdd(&a.rcnt[pid], (u64)full << (a.out_pbl - kRunLog));
                 cur[b] = fresh(nbase[b] + k - 1);
                 fill[b] = f + c - (k << a.out_pbl);
             } else {
@@ -720,22 +867,29 @@ __global__ __launch_bounds__(kPassThreads) void k_pass(PassArgs a) {
     }
 }
 
-// Bucket id ranges of a pass's workgroups (one block, G <= 1024): workgroup
+// Bucket id ranges of a pass's workgroups (block 0, G <= 1024): workgroup
 // w gets ceil(rows_w / PB) + segs_w * F + 1 ids, rows_w <= its tiles * kTile
 // and segs_w the segments its tiles span.  A bin's rows of one segment run
 // fill ceil(r / PB) <= r / PB + 1 buckets (a bucket is only taken for rows),
 // so the range never runs out.  *nb = the ids handed out (listing bound).
-__global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, unsigned G, unsigned *wstart) {
+__global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, unsigned G, unsigned *wstart, u64 *zero_a,
+                                                  u64 *zero_b, u64 zero_n) {
     __shared__ u64 wsum[16];
+    // every block: zero the listing's run counts and cursors (P + 1 each)
+    for (u64 i = (u64)blockIdx.x * 1024 + threadIdx.x; i < zero_n; i += (u64)gridDim.x * 1024) {
+        zero_a[i] = 0ull;
+        zero_b[i] = 0ull;
+    }
+    if (blockIdx.x != 0) return;
     const unsigned w = threadIdx.x;
-    const unsigned T_ = bucketed ? a.tile_start[a.nseg] : (unsigned)((a.n + kTile - 1) / kTile);
+    const unsigned T_ = bucketed ? a.tile_start[a.nseg] : (unsigned)((a.n + a.tile_rows - 1) / a.tile_rows);
     u64 q = 0;
     if (w < G) {
         const unsigned t0 = (unsigned)((u64)w * T_ / G), t1 = (unsigned)((u64)(w + 1) * T_ / G);
         if (t1 > t0) {
             const u64 segs = bucketed ? (u64)(a.tdesc[t1 - 1].seg - a.tdesc[t0].seg + 1) : 1ull;
             const u64 PB = 1ull << a.out_pbl;
-            q = ((u64)(t1 - t0) * kTile + PB - 1) / PB + segs * (1ull << a.fbits) + 1;
+            q = ((u64)(t1 - t0) * a.tile_rows + PB - 1) / PB + segs * (1ull << a.fbits) + 1;
         }
     }
     u64 tot;
@@ -744,55 +898,91 @@ __global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, uns
     if (w == G) *a.nb = (unsigned)(tot < a.max_buckets ? tot : a.max_buckets);
 }
 
-// Runs by partition: count the runs of every bucket per partition,
-// exclusive scan (k_scan_*), then place each bucket's runs at its
-// partition's cursor.  Blocks aggregate in LDS first when partitions are
-// few (pass 1: 512).
+// A bucketed pass's plan in ONE launch (chunk_map + k_tile_desc + k_id_plan
+// + the listing's zeroing: five launches before), for nseg <= kPlanSegs.
+// Every block loads the input set's run starts (nseg + 1) and scans their
+// tile counts (ceil(runs / 64)) in LDS; block 0 writes the tile starts and
+// the workgroups' bucket id ranges (k_id_plan's rule), all blocks write the
+// tile descriptors (grid-strided; a tile's segment by binary search over the
+// starts in LDS) and zero the next listing's counters.
+constexpr int kPlanSegs = 4096;
+__global__ __launch_bounds__(1024) void k_tile_plan(PassArgs a, const u64 *rstart, unsigned G, unsigned tb,
+                                                    unsigned *tile_start, TileDesc *desc, unsigned *wstart, u64 *zero_a,
+                                                    u64 *zero_b, u64 zero_n) {
+    __shared__ unsigned ts[kPlanSegs + 1];
+    __shared__ u64 wsum[16];
+    constexpr int PER = kPlanSegs / 1024;
+    const int nseg = a.nseg;
+    const unsigned rpt = a.tile_rows >> kRunLog;   // runs per tile
+    unsigned c[PER], sum = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int sg = threadIdx.x * PER + i;
+        c[i] = sg < nseg ? (unsigned)((rstart[sg + 1] - rstart[sg] + rpt - 1) / rpt) : 0u;
+        sum += c[i];
+    }
+    u64 total;
+    u64 run = block_excl_scan<1024>(sum, wsum, &total);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int sg = threadIdx.x * PER + i;
+        if (sg < nseg) ts[sg] = (unsigned)run;
+        run += c[i];
+    }
+    if (threadIdx.x == 0) ts[nseg] = (unsigned)total;
+    __syncthreads();
+    const unsigned T = (unsigned)total;
+    // segment of tile t: the last sg with ts[sg] <= t (ts[nseg] = T > t)
+    auto seg_of_tile = [&](unsigned t) -> unsigned {
+        unsigned lo = 0, hi = (unsigned)nseg;   // ts[lo] <= t < ts[hi]
+        while (hi - lo > 1) {
+            const unsigned mid = (lo + hi) >> 1;
+            if (ts[mid] <= t) lo = mid;
+            else hi = mid;
+        }
+        return lo;
+    };
+    for (unsigned t = blockIdx.x * 1024 + threadIdx.x; t < T && t < tb; t += gridDim.x * 1024) {
+        const unsigned sg = seg_of_tile(t);
+        const u64 lo = rstart[sg] + (u64)(t - ts[sg]) * rpt;
+        const u64 e = rstart[sg + 1];
+        TileDesc d;
+        d.lo = lo;
+        d.cnt = (unsigned)(e - lo < (u64)rpt ? e - lo : (u64)rpt);
+        d.seg = sg;
+        desc[t] = d;
+    }
+    for (u64 i = (u64)blockIdx.x * 1024 + threadIdx.x; i < zero_n; i += (u64)gridDim.x * 1024) {
+        zero_a[i] = 0ull;
+        zero_b[i] = 0ull;
+    }
+    if (blockIdx.x != 0) return;
+    for (int sg = threadIdx.x; sg <= nseg; sg += 1024) tile_start[sg] = ts[sg];
+    const unsigned w = threadIdx.x;
+    u64 q = 0;
+    if (w < G) {
+        const unsigned t0 = (unsigned)((u64)w * T / G), t1 = (unsigned)((u64)(w + 1) * T / G);
+        if (t1 > t0) {
+            const u64 segs = (u64)(seg_of_tile(t1 - 1) - seg_of_tile(t0) + 1);
+            const u64 PB = 1ull << a.out_pbl;
+            q = ((u64)(t1 - t0) * a.tile_rows + PB - 1) / PB + segs * (1ull << a.fbits) + 1;
+        }
+    }
+    u64 tot;
+    const u64 pre = block_excl_scan<1024>(q, wsum, &tot);
+    if (w <= G) wstart[w] = (unsigned)(pre < a.max_buckets ? pre : a.max_buckets);
+    if (w == G) *a.nb = (unsigned)(tot < a.max_buckets ? tot : a.max_buckets);
+}
+
+// Runs by partition: the pass counted every bucket's runs per partition
+// (PassArgs::rcnt), an exclusive scan (scan_one) gives the partitions'
+// starts, then k_bplace places each bucket's runs at its partition's cursor.
+// Blocks aggregate in LDS first when partitions are few (pass 1: 512).
+// Buckets [0, *nb) of a pass, clamped to the set's capacity; holes (unused
+// ids of a workgroup's range) are kNoBucket.
 constexpr int kListPer = 4;   // (1 or 2 per thread: within 10 %)
 constexpr int kListLds = 4096;
 
-__device__ __forceinline__ unsigned runs_of(unsigned fill) { return (fill + (1u << kRunLog) - 1) >> kRunLog; }
-
-// Buckets [0, *nb) of a pass, clamped to the set's capacity; holes (unused
-// ids of a workgroup's range) are kNoBucket.
-__global__ __launch_bounds__(1024) void k_bcount(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, u64 *rcnt, int P) {
-    __shared__ unsigned cr[kListLds];
-    const unsigned n = *nb < max_buckets ? *nb : max_buckets;
-    const u64 base = (u64)blockIdx.x * 1024 * kListPer;
-    if (base >= n) return;
-    const bool lds = P <= kListLds;
-    if (lds)
-        for (int i = threadIdx.x; i < P; i += 1024) cr[i] = 0u;
-    __syncthreads();
-    const unsigned lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int i = 0; i < kListPer; ++i) {
-        const u64 j = base + (u64)i * 1024 + threadIdx.x;
-        const unsigned b = j < n ? bbin[j] : kNoBucket;
-        const bool valid = b < (unsigned)P;
-        const unsigned nr = valid ? runs_of(bfill[j]) : 0u;
-        if (lds) {
-            if (valid) atomicAdd(&cr[b], nr);
-            continue;
-        }
-        // the wave's lanes that hold the same partition as its first valid
-        // lane add once (a skewed key's buckets are consecutive ids: C4's hot
-        // partition put ~10^4 same-address atomics on one counter, 0.11 ms)
-        const u64 vm = __ballot(valid);
-        if (!vm) continue;   // uniform
-        const int l0 = __ffsll((long long)vm) - 1;
-        const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)b, l0);
-        const bool same = valid && b == b0;
-        const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)wave_incl_add(same ? nr : 0u), 63);
-        if (valid && !same) atomicAdd(&rcnt[b], (u64)nr);
-        if ((int)lane == l0) atomicAdd(&rcnt[b0], (u64)tot);
-    }
-    if (!lds) return;
-    __syncthreads();
-    for (int i = threadIdx.x; i < P; i += 1024)
-        if (cr[i]) atomicAdd(&rcnt[i], (u64)cr[i]);
-}
 
 __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
                                                  unsigned max_buckets, int pbl, const u64 *rstart, u64 *rcur,
@@ -1000,8 +1190,9 @@ struct ItemDesc {
 __global__ __launch_bounds__(256) void k_item_desc(const unsigned *work_start, const unsigned *work_owner,
                                                    const u64 *s_rstart, const u64 *r_rstart, int P, unsigned chr,
                                                    ItemDesc *desc, unsigned *zero, unsigned *zero2, unsigned *zero3,
-                                                   const u64 *split) {
+                                                   const u64 *split, u64 *zero_count) {
     const unsigned w = blockIdx.x * 256 + threadIdx.x;
+    if (w == 0 && zero_count) *zero_count = 0ull;   // the join's output counter (no memset launch)
     if (w == 0 && zero) *zero = 0u;
     if (w == 0 && zero2) *zero2 = 0u;
     if (w == 0 && zero3) *zero3 = 0u;
@@ -1518,8 +1709,18 @@ __device__ __forceinline__ ItemDesc sload(const ItemDesc *p) {
 // form of the collision walks, every row's CAS in flight at once, measured
 // slower: C3 join 2.75 -> 2.99 ms; so was a walk reading the aligned slot
 // pair ahead and CASing only an EMPTY slot: narrow 1.85 -> 2.25 ms)
+template <bool WIDE, int TSL, int NT, int SI>
+struct JoinUSmem {
+    u64 tkey[1 << TSL];
+    u64 tpay[WIDE ? (1 << TSL) : 1];
+    u64 s_base;
+    unsigned s_bad, s_dup, s_rows;
+    unsigned s_cw[SI * (NT / 64)];
+    u64 wsum[16];
+};
+
 template <bool WIDE, bool WRITE, int TSL, int NT, int RI, int SI, int WPS, bool GEN = true, int ABL = 0>
-__global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
+__device__ __forceinline__ void join_u_body(JoinArgs a, JoinUSmem<WIDE, TSL, NT, SI> &sm) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     typedef typename std::conditional<WIDE, u64, unsigned>::type PT;
@@ -1537,12 +1738,14 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     constexpr unsigned rmax_rows = (unsigned)(TS * 3 / 4);
     static_assert(NT % 64 == 0 && rb <= rmax, "one round must fit the table");
     constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
-    __shared__ u64 tkey[TS];
-    __shared__ u64 tpay[WIDE ? TS : 1];
-    __shared__ u64 s_base;
-    __shared__ unsigned s_bad, s_dup, s_rows;
-    __shared__ unsigned s_cw[SI * NW];
-    __shared__ u64 wsum[16];
+    auto &tkey = sm.tkey;
+    auto &tpay = sm.tpay;
+    auto &s_base = sm.s_base;
+    auto &s_bad = sm.s_bad;
+    auto &s_dup = sm.s_dup;
+    auto &s_rows = sm.s_rows;
+    auto &s_cw = sm.s_cw;
+    auto &wsum = sm.wsum;
     bool dup_sent = false;   // this workgroup has set a.dup_flag
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
@@ -1838,6 +2041,12 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
     }
 }
 
+template <bool WIDE, bool WRITE, int TSL, int NT, int RI, int SI, int WPS, bool GEN = true, int ABL = 0>
+__global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
+    __shared__ JoinUSmem<WIDE, TSL, NT, SI> sm;
+    join_u_body<WIDE, WRITE, TSL, NT, RI, SI, WPS, GEN, ABL>(a, sm);
+}
+
 // k_join_b: k_join_u's item loop, loads, defer rules and output compaction
 // over a BUCKETED LDS table (4 slots per bucket, 1024 buckets, a count per
 // bucket) instead of linear probing -- wide rows, the fast shape
@@ -1872,8 +2081,28 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 // i32 rows keep keys and row ids apart (a bucket's keys are one 16-B read);
 // an item whose probe rows would write many pairs per row (the reference's
 // keys in [1, 100k]) goes to k_join_grp before anything of it is written.
+// the int64 rows' fast join shape (see "join shapes" below)
+constexpr int kFastNTc = 768, kFastRIc = 3, kFastSIc = 3, kFastWPSc = 6;
+
+template <bool WIDE, int NT, int SI, bool DETECT, int TSL>
+struct JoinBSmem {
+    static constexpr int TS = 1 << TSL, NB = TS / 4, NW = NT / 64;
+    static constexpr unsigned kSusCap = 512;
+    alignas(16) u64 tkey[TS];
+    alignas(16) u64 tpay[WIDE ? TS : 2];
+    alignas(16) unsigned bcnt[NB];
+    alignas(16) unsigned bsig[DETECT ? NB : 4];
+    unsigned sus[DETECT ? kSusCap : 1];
+    u64 s_base;
+    alignas(16) unsigned s_ctl[4];
+    unsigned s_cw[SI * NW + NW];
+    unsigned s_skip;
+    unsigned s_mpre[NT];
+    unsigned s_next;
+};
+
 template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false, int TSL = 12>
-__global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
+__device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, DETECT, TSL> &sm) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
     typedef typename std::conditional<WIDE, u64, unsigned>::type PT;
@@ -1891,21 +2120,21 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     // a bucket's word: its count (rows stored in it or passed it, <= 4096) in
     // the low half, the overflow bits of the keys stored past it in the high
     constexpr unsigned kCntMask = 0xFFFFu;
-    __shared__ __attribute__((aligned(16))) u64 tkey[TS];
-    __shared__ __attribute__((aligned(16))) u64 tpay[WIDE ? TS : 2];
-    __shared__ __attribute__((aligned(16))) unsigned bcnt[NB];
+    auto &tkey = sm.tkey;
+    auto &tpay = sm.tpay;
+    auto &bcnt = sm.bcnt;
     // (DETECT) per home bucket the OR of its rows' 1-of-32 key signatures,
     // and the suspect slots: slot | home bucket << 16
-    constexpr unsigned kSusCap = 512;
-    __shared__ __attribute__((aligned(16))) unsigned bsig[DETECT ? NB : 4];
-    __shared__ unsigned sus[DETECT ? kSusCap : 1];
-    __shared__ u64 s_base;
-    __shared__ __attribute__((aligned(16))) unsigned s_ctl[4];   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
+    constexpr unsigned kSusCap = JoinBSmem<WIDE, NT, SI, DETECT, TSL>::kSusCap;
+    auto &bsig = sm.bsig;
+    auto &sus = sm.sus;
+    auto &s_base = sm.s_base;
+    auto &s_ctl = sm.s_ctl;   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
     unsigned &s_bad = s_ctl[0], &s_dup = s_ctl[1], &s_rows = s_ctl[2], &s_nsus = s_ctl[3];
     // per (row slot, wave) ballot counts, then per wave the multi rows' pairs
-    __shared__ unsigned s_cw[SI * NW + NW];
-    __shared__ unsigned s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
-    __shared__ unsigned s_mpre[NT];   // a thread's multi pairs before it in its wave (kept out of registers)
+    auto &s_cw = sm.s_cw;
+    auto &s_skip = sm.s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
+    auto &s_mpre = sm.s_mpre;   // a thread's multi pairs before it in its wave (kept out of registers)
     // a.next_item (i32 rows; int64 rows and DETECT walk w += grid: the wide
     // instantiation has no SGPRs left for it, its next item's run entries
     // already fill them -- with the claim it spilled 20 B and lost 6 % on C3
@@ -1913,7 +2142,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     // item of iteration k + 2 into s_next after its first barrier, and the top
     // of iteration k + 1 reads it (a workgroup's first two items are static:
     // blockIdx.x, blockIdx.x + grid)
-    __shared__ unsigned s_next;
+    auto &s_next = sm.s_next;
     bool dup_sent = false;
 
     const unsigned total = __builtin_amdgcn_readfirstlane(a.work_start[a.P]);
@@ -2322,6 +2551,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
     }
 }
 
+template <bool WIDE, bool WRITE, int NT, int RI, int SI, int WPS, bool DETECT = false, int TSL = 12>
+__global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
+    __shared__ JoinBSmem<WIDE, NT, SI, DETECT, TSL> sm;
+    join_b_body<WIDE, WRITE, NT, RI, SI, WPS, DETECT, TSL>(a, sm);
+}
+
+
 // --------------------------------------------------------------- grouped join
 // k_join_grp: narrow rows (the reference's i32 keys / row ids) whose build
 // keys repeat many times -- join-performances.md:3-6's 10M x 10M keys in
@@ -2560,7 +2796,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
 // Fast shape: 768 threads, 3 build + 3 probe rows per thread, 6 waves per
 // SIMD (profiles/r02_join_fast.txt: C3 k_join 3.50 -> 2.81 ms, C2 12.34 ->
 // 9.45 ms, C1-ref 1.31 -> 0.96 ms; k_join_b: C3 2.77 -> 2.55 ms).
-constexpr int kFastNT = 768, kFastRI = 3, kFastSI = 3, kFastWPS = 6;
+constexpr int kFastNT = kFastNTc, kFastRI = kFastRIc, kFastSI = kFastSIc, kFastWPS = kFastWPSc;
 // probe sides much larger than the build side (C2: 2^30 x 2^20, ~1000 S rows
 // per R row): many sub-chunks per item, so bigger sub-chunks and more waves
 // (1024 threads x 4 S rows, 8 waves per SIMD): C2 join 9.45 -> 8.77 ms, C3
@@ -2603,11 +2839,44 @@ unsigned pass_grid(u64 n) {
     return (unsigned)(g < cus ? g : cus);
 }
 
+// The k_pass variant of a pass of fb bits: passes of <= 8 bits run the
+// half-size workgroups, two per CU (kSmallPassThreads).
+inline bool small_pass(int fb) { return fb <= 8; }
+inline unsigned pass_tile_rows(int fb) { return small_pass(fb) ? (unsigned)(kSmallPassThreads * kPassRows) : (unsigned)kTile; }
+unsigned pass_grid(u64 n, int fb) {
+    if (!small_pass(fb)) return pass_grid(n);
+    const u64 tiles = (n + pass_tile_rows(fb) - 1) / pass_tile_rows(fb);
+    const u64 g = tiles / 8 > 0 ? tiles / 8 : 1;
+    const u64 w = 2ull * (u64)cu_count();
+    return (unsigned)(g < w ? g : w);
+}
+
 // Exclusive scan of a u64 array of len elements in place (k_scan_*).
 void scan_u64(u64 *v, u64 len, u64 *sums, hipStream_t st) {
     const unsigned nb = blocks_for(len, kScanBlock);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, st, v, len, sums);
     if (nb > 1) hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, st, v, len, (const u64 *)sums);
+}
+
+// Exclusive scan of len u64 in place in one launch: one block, or the
+// look-back scan over ws.scan_state.
+void scan_one(u64 *v, u64 len, const RadixWork &ws, hipStream_t st) {
+    if (len <= (u64)kScanBlock) {
+        hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, st, v, len, ws.scan_sums);
+        return;
+    }
+    hipLaunchKernelGGL((k_scan_lb<false>), dim3(blocks_for(len, kLbTile)), dim3(kLbThreads), 0, st, v, len,
+                       ws.scan_state, ChunkMapArgs{});
+}
+
+// chunk_map in one launch (k_scan_lb's MAP mode): start[0..nseg], owner[],
+// and the count scan (split order) in ws.pcur.
+void chunk_map_one(const u64 *off_a, const u64 *off_b, int nseg, unsigned chunk, unsigned *start, unsigned *owner,
+                   const RadixWork &ws, hipStream_t st, bool split = false) {
+    ChunkMapArgs m{off_a, off_b, chunk, split, start, owner};
+    const u64 n = (u64)nseg + 1;
+    hipLaunchKernelGGL((k_scan_lb<true>), dim3(blocks_for(n, kLbTile)), dim3(kLbThreads), 0, st, ws.pcur, n,
+                       ws.scan_state, m);
 }
 
 // per_seg: about how many chunks a segment has (sizes the owner fill's
@@ -2659,9 +2928,10 @@ RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
         // k_id_plan's ranges: sum over workgroups of ceil(tiles_w * kTile /
         // PB) + segs_w * F + 1, with sum segs_w <= nseg + G; tiles of a
         // bucketed pass <= runs / 64 + nseg, runs <= rows / 64 + buckets_in
-        const u64 G = pass_grid(rows);
-        const u64 tiles = i == 0 ? (rows + kTile - 1) / kTile : (rows / 64 + prev_b) / 64 + nseg + 1;
-        const u64 b = (tiles * kTile >> pl.pbl[i]) + G + (nseg + G) * F + G + 1;
+        const u64 G = pass_grid(rows, pl.bits[i]);
+        const u64 tr = pass_tile_rows(pl.bits[i]), rpt = tr >> kRunLog;
+        const u64 tiles = i == 0 ? (rows + tr - 1) / tr : (rows / 64 + prev_b) / rpt + nseg + 1;
+        const u64 b = (tiles * tr >> pl.pbl[i]) + G + (nseg + G) * F + G + 1;
         prev_b = b;
         if (to_final == final_set) {
             if (b > need.buckets) need.buckets = b;
@@ -2673,9 +2943,10 @@ RadixNeed radix_need(long long n, const RadixPlan &pl, bool final_set) {
 }
 
 unsigned long long radix_tiles(long long n, int max_nseg) {
-    // bucketed tiles: kTile / 64 runs each, <= one partial tile per segment;
-    // every run holds >= 1 row, so runs <= n (the bound is loose but small)
-    return (u64)(n > 0 ? n : 1) / (kTile >> kRunLog) + (u64)max_nseg + 2;
+    // bucketed tiles: >= kSmallPassThreads * kPassRows / 64 runs each (the
+    // smaller variant), <= one partial tile per segment; every run holds >= 1
+    // row, so runs <= n (the bound is loose but small)
+    return (u64)(n > 0 ? n : 1) / ((kSmallPassThreads * kPassRows) >> kRunLog) + (u64)max_nseg + 2;
 }
 
 size_t radix_item_desc_bytes() { return sizeof(ItemDesc); }
@@ -2787,7 +3058,7 @@ hipError_t radix_route(const SrcDev &src, int rbits, void *out_tuples, unsigned 
     a.out_pbl = 0;
     a.shift = 64 - rbits;
     a.fbits = rbits;
-    a.zero_n = 0;
+    a.rcnt = nullptr;
     a.slot_base = (const u64 *)hist;
     a.out_max_rows = n;
     if (src.form == kCols64) hipLaunchKernelGGL((k_slot_hist<true, kCols64>), dim3(G), dim3(1024), 0, st, a, (u64 *)hist);
@@ -2807,9 +3078,10 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
                         int nseg, const RadixWork &ws, const BucketSet &out, hipStream_t st) {
     int shift = 64 - pl.skip;
     for (int pass = 0; pass < first; ++pass) shift -= pl.bits[pass];
-    const unsigned grid = pass_grid(n > 0 ? n : 1);
     for (int pass = first; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
+        const unsigned grid = pass_grid(n > 0 ? n : 1, fb);
+        const bool small = small_pass(fb);
         shift -= fb;
         const BucketSet &dst = ((pl.passes - 1 - pass) % 2) == 0 ? out : ws.tmp;
         PassArgs a;
@@ -2837,29 +3109,48 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         a.out_pbl = pl.pbl[pass];
         a.shift = shift;
         a.fbits = fb;
+        a.tile_rows = pass_tile_rows(fb);
         hipError_t e = hipSuccess;
-        if (prev) {
-            // tiles of kTile / 64 runs per segment, tile -> segment, and one
-            // descriptor per tile
-            chunk_map(prev->rstart, nullptr, nseg, (unsigned)(kTile >> kRunLog), ws.tile_start, ws.tile_owner, ws.pcur,
-                      ws.scan_sums, st, (u64)n / (u64)(nseg > 0 ? nseg : 1) / (u64)kTile);
-            const u64 tb = radix_tiles((long long)n, nseg);
-            hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, st, (const unsigned *)ws.tile_start,
-                               (const unsigned *)ws.tile_owner, (const u64 *)prev->rstart, nseg, (unsigned)tb,
-                               (TileDesc *)ws.tdesc);
-            a.tdesc = (const TileDesc *)ws.tdesc;
-        }
         a.wstart = ws.wstart;
-        // list the runs by partition afterwards: rstart = scan of the
-        // per-partition run counts, k_bplace's cursors rstart + rcur
+        // the pass counts its buckets' runs per partition into dst.rstart;
+        // the plan kernel zeroes them and k_bplace's cursors first
         const u64 P = (u64)nseg << fb;
-        a.zero_a = dst.rstart;
-        a.zero_b = ws.rcur;
-        a.zero_n = n > 0 ? P + 1 : 0;
-        if (grid > 1024) return hipErrorInvalidValue;   // k_id_plan: one block
-        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, st, a, prev != nullptr, grid, ws.wstart);
+        a.rcnt = n > 0 ? dst.rstart : nullptr;
+        if (grid > 1023) return hipErrorInvalidValue;   // plans: one thread per workgroup + 1
+        const unsigned zgrid = blocks_for(P + 1, 1024);
+        if (prev && nseg <= kPlanSegs) {
+            // tile map, descriptors, id ranges and zeroing in one launch
+            const u64 tb = radix_tiles((long long)n, nseg);
+            a.tdesc = (const TileDesc *)ws.tdesc;
+            unsigned pg = blocks_for(tb, 1024);
+            if (pg < zgrid) pg = zgrid;
+            if (pg > 1024) pg = 1024;
+            hipLaunchKernelGGL(k_tile_plan, dim3(pg), dim3(1024), 0, st, a, (const u64 *)prev->rstart, grid, (unsigned)tb,
+                               ws.tile_start, (TileDesc *)ws.tdesc, ws.wstart, dst.rstart, ws.rcur, P + 1);
+        } else {
+            if (prev) {
+                // tiles of kTile / 64 runs per segment, tile -> segment, and one
+                // descriptor per tile
+                const unsigned rpt = a.tile_rows >> kRunLog;
+                chunk_map(prev->rstart, nullptr, nseg, rpt, ws.tile_start, ws.tile_owner, ws.pcur, ws.scan_sums, st,
+                          (u64)n / (u64)(nseg > 0 ? nseg : 1) / (u64)a.tile_rows);
+                const u64 tb = radix_tiles((long long)n, nseg);
+                hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, st,
+                                   (const unsigned *)ws.tile_start, (const unsigned *)ws.tile_owner,
+                                   (const u64 *)prev->rstart, nseg, (unsigned)tb, (TileDesc *)ws.tdesc, rpt);
+                a.tdesc = (const TileDesc *)ws.tdesc;
+            }
+            hipLaunchKernelGGL(k_id_plan, dim3(zgrid < 1024 ? zgrid : 1024), dim3(1024), 0, st, a, prev != nullptr, grid,
+                               ws.wstart, dst.rstart, ws.rcur, P + 1);
+        }
         if (n > 0) {
-#define HJ_PASS(W, FORM) hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a)
+#define HJ_PASS(W, FORM)                                                                                    \
+    do {                                                                                                    \
+        if (small)                                                                                          \
+            hipLaunchKernelGGL((k_pass<W, FORM, 0, false, kSmallPassThreads, kSmallFan>), dim3(grid),       \
+                               dim3(kSmallPassThreads), 0, st, a);                                          \
+        else hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a);               \
+    } while (0)
             if (prev) {
                 if (wide) HJ_PASS(true, kBucketed);
                 else HJ_PASS(false, kBucketed);
@@ -2872,17 +3163,10 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
             }
 #undef HJ_PASS
         }
-        if (n <= 0) {
-            e = hipMemsetAsync(dst.rstart, 0, (P + 1) * sizeof(u64), st);
-            if (e == hipSuccess) e = hipMemsetAsync(ws.rcur, 0, (P + 1) * sizeof(u64), st);
-            if (e != hipSuccess) return e;
-        }
         // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
         if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
         const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
-        hipLaunchKernelGGL(k_bcount, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, dst.rstart, (int)P);
-        scan_u64(dst.rstart, P + 1, ws.scan_sums, st);
+        scan_one(dst.rstart, P + 1, ws, st);
         hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
                            (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass],
                            (const u64 *)dst.rstart, ws.rcur, dst.runs, (int)P);
@@ -2992,8 +3276,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     // heavy-first item order: int64 rows (static item striding); i32 rows
     // claim items dynamically and k_join_grp lost 0.2 ms on REF-A with it
     const bool heavy_first = kHeavyFirst && wide;
-    chunk_map(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws.pcur, ws.scan_sums, st, 1,
-              heavy_first);
+    chunk_map_one(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws, st, heavy_first);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
     // the deferred-item lists live after the work map: the fast kernels'
     // (for k_join, or for k_join_grp with i32 rows), then k_join_grp's
@@ -3003,7 +3286,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
                        (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n, next_item,
-                       heavy_first ? (const u64 *)ws.pcur : nullptr);
+                       heavy_first ? (const u64 *)ws.pcur : nullptr, counter);
     JoinArgs a;
     a.r = r.rows;
     a.s = s.rows;
@@ -3038,7 +3321,9 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                   (k_join_u<true, false, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), kStreamNT);
         } else {
             // k_join_b unless most build keys repeat (its multi-match walks
-            // lose to k_join_u's per-row walks there)
+            // lose to k_join_u's per-row walks there).  (Both bodies in one
+            // kernel, the sample choosing, spilled 20 B at the 80-VGPR cap of
+            // 6 waves per SIMD: the unchosen kernel's exit launch stays.)
             a.modes = kModeUnique | kModeSome;
             HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
@@ -3096,11 +3381,11 @@ hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, con
     const int P = 1 << pl.total_bits;
     unsigned *work_owner = work_start + P + 1;
     const unsigned whole = 0x7FFFFFFFu;   // runs per item: a partition is one item
-    chunk_map(r.rstart, r.rstart, P, whole, work_start, work_owner, ws.pcur, ws.scan_sums, st);
+    chunk_map_one(r.rstart, r.rstart, P, whole, work_start, work_owner, ws, st);
     unsigned *defer_n = work_owner + radix_join_items(pl, 0);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for((u64)P + 1, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)r.rstart, (const u64 *)r.rstart, P, whole,
-                       (ItemDesc *)desc, defer_n, nullptr, nullptr, nullptr);
+                       (ItemDesc *)desc, defer_n, nullptr, nullptr, nullptr, nullptr);
     JoinArgs a{};
     a.r = r.rows;
     a.s = r.rows;

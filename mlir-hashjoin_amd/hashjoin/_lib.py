@@ -50,6 +50,7 @@ def _load():
         "hj_last_error": (C.c_char_p, []),
         "hj_device_info": (_int, [_int, C.POINTER(_i64)]),
         "hj_host_memo_hits": (_i64, []),
+        "hj_host_set_reuse": (_int, [_int]),
         "hj_ctx_create": (_vp, [_int]),
         "hj_ctx_destroy": (None, [_vp]),
         "hj_ctx_reserve": (_int, [_vp, _i64, _int]),

@@ -78,6 +78,7 @@ class HashJoin:
         check(lib.hj_ctx_set_strategy(self._ctx, STRATEGIES[name]), "hj_ctx_set_strategy")
         check(lib.hj_ctx_set_radix_bits(self._ctx, int(radix_bits)), "hj_ctx_set_radix_bits")
 
+    @property
     def strategy_used(self):
         return {HJ_STRATEGY_GLOBAL: "global", HJ_STRATEGY_RADIX: "radix"}.get(
             lib.hj_ctx_strategy_used(self._ctx), None)

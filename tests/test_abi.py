@@ -88,6 +88,21 @@ def test_header_compiles_as_c():
     assert r.returncode == 0, r.stderr
 
 
+def test_reuse_mode_setter():
+    """hj_host_set_reuse (host only): returns the previous mode, rejects
+    unknown ones and leaves the mode unchanged then."""
+    import hashjoin
+    L = hashjoin.lib
+    prev = L.hj_host_set_reuse(1)
+    try:
+        assert prev in (0, 1, 2)
+        assert L.hj_host_set_reuse(2) == 1
+        assert L.hj_host_set_reuse(7) == hashjoin._lib.HJ_ERR_ARG
+        assert L.hj_host_set_reuse(0) == 2
+    finally:
+        L.hj_host_set_reuse(prev)
+
+
 def test_route_plan_host():
     """The folded routing's bin bits (host function, no device needed): 9 -
     log2(ranks) bits below the owner bits while the local build side is

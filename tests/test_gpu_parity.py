@@ -156,6 +156,45 @@ def test_memref_count_then_probe_reuses_the_join(oracle):
     assert oracle.same_multiset(o_r, o_s, *exp5)
 
 
+@pytest.mark.parametrize("mode", ["exact", "off"])
+def test_memref_reuse_modes(oracle, mode):
+    """hj_host_set_reuse: EXACT reuses only byte-identical inputs (a host copy
+    kept by the count, compared with memcmp), OFF never reuses; both deliver
+    the join of the probe's own inputs."""
+    L = hashjoin.lib
+    prev = L.hj_host_set_reuse({"exact": 1, "off": 2}[mode])
+    try:
+        rk, rp, sk, sp = oracle.gen_pkfk_i64(31, 6000, 9000, 0.7)
+        h0 = L.hj_host_memo_hits()
+        m = MR.count_i64(rk, rp, sk, sp)
+        o_r = np.empty(m, np.int64); o_s = np.empty(m, np.int64)
+        assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+        assert L.hj_host_memo_hits() == h0 + (1 if mode == "exact" else 0)
+        assert oracle.same_multiset(o_r, o_s, *oracle.nested_loop_i64(rk, rp, sk, sp))
+        # one payload byte changed between count and probe: never reused
+        h1 = L.hj_host_memo_hits()
+        m = MR.count_i64(rk, rp, sk, sp)
+        sp[4321] ^= 1 << 40
+        exp = oracle.nested_loop_i64(rk, rp, sk, sp)
+        o_r = np.empty(len(exp[0]), np.int64); o_s = np.empty(len(exp[0]), np.int64)
+        assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+        assert L.hj_host_memo_hits() == h1
+        assert oracle.same_multiset(o_r, o_s, *exp)
+        # strided i32 memrefs, unchanged: reused under EXACT
+        base_r = oracle.gen_uniform_i32(32, 1, 1, 50, 4000)
+        base_s = oracle.gen_uniform_i32(32, 2, 1, 50, 3000)
+        r = base_r[3:3603:3]; s = base_s[1:2401:2]
+        h2 = L.hj_host_memo_hits()
+        m = MR.count_i32(r, s, base_r, base_s)
+        o_r = np.empty(m, np.int32); o_s = np.empty(m, np.int32)
+        assert MR.probe_i32(r, s, o_r, o_s) == 0
+        assert L.hj_host_memo_hits() == h2 + (1 if mode == "exact" else 0)
+        assert oracle.same_multiset(o_r, o_s, *oracle.nested_loop_i32(np.ascontiguousarray(r),
+                                                                       np.ascontiguousarray(s)))
+    finally:
+        L.hj_host_set_reuse(prev)
+
+
 def test_memref_concurrent_host_threads(oracle):
     """Host entry points share one default context: concurrent callers are
     serialised by its lock, each gets its own join."""
