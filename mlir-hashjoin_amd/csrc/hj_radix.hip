@@ -431,11 +431,11 @@ __device__ __forceinline__ bool tile_row(const PassArgs &a, u64 lo, unsigned v, 
 // give the bases): rows land grouped by bin with no holes, so a bin's rows
 // can be sent as one message.  A slot's first line is shared with the slot
 // before it (written partly, once); every other line is written whole.
-template <bool WIDE, int FORM, int ABL = 0, bool EXACT = false, int NT = kPassThreads, int FMAX = kMaxFan>
+template <bool WIDE, int FORM, int ABL = 0, bool EXACT = false, int NT = kPassThreads, int FMAX = kMaxFan,
+          int IT = kPassRows>
 __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
     typedef Row<WIDE> R;
     typedef typename R::T T;
-    constexpr int IT = kPassRows;
     constexpr int kTile = NT * IT;          // (shadows the file's: this variant's tile)
     constexpr int kPassThreads = NT;
     constexpr int kMaxFan = FMAX;
@@ -906,9 +906,27 @@ __global__ __launch_bounds__(1024) void k_id_plan(PassArgs a, bool bucketed, uns
 // tile descriptors (grid-strided; a tile's segment by binary search over the
 // starts in LDS) and zero the next listing's counters.
 constexpr int kPlanSegs = 4096;
-__global__ __launch_bounds__(1024) void k_tile_plan(PassArgs a, const u64 *rstart, unsigned G, unsigned tb,
-                                                    unsigned *tile_start, TileDesc *desc, unsigned *wstart, u64 *zero_a,
-                                                    u64 *zero_b, u64 zero_n) {
+struct TilePlanArgs {
+    PassArgs a;
+    const u64 *rstart;
+    unsigned G, tb;
+    unsigned *tile_start;
+    TileDesc *desc;
+    unsigned *wstart;
+    u64 *zero_a, *zero_b;
+    u64 zero_n;
+};
+
+// (block bid of nblk: the body of k_tile_plan, or of k_place_plan's plan blocks)
+__device__ __forceinline__ void tile_plan_body(const TilePlanArgs &p, unsigned bid, unsigned nblk) {
+    const PassArgs &a = p.a;
+    const u64 *rstart = p.rstart;
+    const unsigned G = p.G, tb = p.tb;
+    unsigned *tile_start = p.tile_start;
+    TileDesc *desc = p.desc;
+    unsigned *wstart = p.wstart;
+    u64 *zero_a = p.zero_a, *zero_b = p.zero_b;
+    const u64 zero_n = p.zero_n;
     __shared__ unsigned ts[kPlanSegs + 1];
     __shared__ u64 wsum[16];
     constexpr int PER = kPlanSegs / 1024;
@@ -942,7 +960,7 @@ __global__ __launch_bounds__(1024) void k_tile_plan(PassArgs a, const u64 *rstar
         }
         return lo;
     };
-    for (unsigned t = blockIdx.x * 1024 + threadIdx.x; t < T && t < tb; t += gridDim.x * 1024) {
+    for (unsigned t = bid * 1024 + threadIdx.x; t < T && t < tb; t += nblk * 1024) {
         const unsigned sg = seg_of_tile(t);
         const u64 lo = rstart[sg] + (u64)(t - ts[sg]) * rpt;
         const u64 e = rstart[sg + 1];
@@ -952,11 +970,11 @@ __global__ __launch_bounds__(1024) void k_tile_plan(PassArgs a, const u64 *rstar
         d.seg = sg;
         desc[t] = d;
     }
-    for (u64 i = (u64)blockIdx.x * 1024 + threadIdx.x; i < zero_n; i += (u64)gridDim.x * 1024) {
+    for (u64 i = (u64)bid * 1024 + threadIdx.x; i < zero_n; i += (u64)nblk * 1024) {
         zero_a[i] = 0ull;
         zero_b[i] = 0ull;
     }
-    if (blockIdx.x != 0) return;
+    if (bid != 0) return;
     for (int sg = threadIdx.x; sg <= nseg; sg += 1024) tile_start[sg] = ts[sg];
     const unsigned w = threadIdx.x;
     u64 q = 0;
@@ -974,23 +992,38 @@ __global__ __launch_bounds__(1024) void k_tile_plan(PassArgs a, const u64 *rstar
     if (w == G) *a.nb = (unsigned)(tot < a.max_buckets ? tot : a.max_buckets);
 }
 
+__global__ __launch_bounds__(1024) void k_tile_plan(TilePlanArgs p) { tile_plan_body(p, blockIdx.x, gridDim.x); }
+
 // Runs by partition: the pass counted every bucket's runs per partition
 // (PassArgs::rcnt), an exclusive scan (scan_one) gives the partitions'
 // starts, then k_bplace places each bucket's runs at its partition's cursor.
 // Blocks aggregate in LDS first when partitions are few (pass 1: 512).
 // Buckets [0, *nb) of a pass, clamped to the set's capacity; holes (unused
 // ids of a workgroup's range) are kNoBucket.
-constexpr int kListPer = 4;   // (1 or 2 per thread: within 10 %)
+constexpr int kListPer = 4;   // (1, 2 per thread: within 10 %; 1 again in round 4: r04g)
 constexpr int kListLds = 4096;
 
 
-__global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const unsigned *bfill, const unsigned *nb,
-                                                 unsigned max_buckets, int pbl, const u64 *rstart, u64 *rcur,
-                                                 u64 *runs, int P) {
+struct PlaceArgs {
+    const unsigned *bbin, *bfill, *nb;
+    unsigned max_buckets;
+    int pbl;
+    const u64 *rstart;
+    u64 *rcur, *runs;
+    int P;
+};
+
+__device__ __forceinline__ void bplace_body(const PlaceArgs &pa, unsigned bid) {
+    const unsigned *bbin = pa.bbin, *bfill = pa.bfill, *nb = pa.nb;
+    const unsigned max_buckets = pa.max_buckets;
+    const int pbl = pa.pbl;
+    const u64 *rstart = pa.rstart;
+    u64 *rcur = pa.rcur, *runs = pa.runs;
+    const int P = pa.P;
     __shared__ unsigned cr[kListLds];
     __shared__ u64 cbr[kListLds];
     const unsigned n = *nb < max_buckets ? *nb : max_buckets;
-    const u64 base = (u64)blockIdx.x * 1024 * kListPer;
+    const u64 base = (u64)bid * 1024 * kListPer;
     if (base >= n) return;
     // bucket j's runs: rows (j << pbl) + 64 k, count min(64, fill - 64 k).
     // Called by the whole wave (every lane, `ok` = it holds a bucket): the
@@ -1076,6 +1109,17 @@ __global__ __launch_bounds__(1024) void k_bplace(const unsigned *bbin, const uns
         const bool ok = bn[i] != kNoBucket;
         put_runs(ok, j, fl[i], ok ? cbr[bn[i]] + rr[i] : 0ull);
     }
+}
+
+__global__ __launch_bounds__(1024) void k_bplace(PlaceArgs pa) { bplace_body(pa, blockIdx.x); }
+
+// One launch for two independent steps that both only need the scanned run
+// starts of pass p: pass p's run placement (blocks [0, nplace)) and pass p +
+// 1's plan (the rest).  (They use separate bucket-count words and cursor
+// arrays: the plan zeroes pass p + 1's while pass p's are in use.)
+__global__ __launch_bounds__(1024) void k_place_plan(PlaceArgs pa, unsigned nplace, TilePlanArgs tp) {
+    if (blockIdx.x < nplace) bplace_body(pa, blockIdx.x);
+    else tile_plan_body(tp, blockIdx.x - nplace, gridDim.x - nplace);
 }
 
 // --------------------------------------------------------------- join
@@ -2842,10 +2886,17 @@ unsigned pass_grid(u64 n) {
 // The k_pass variant of a pass of fb bits: passes of <= 8 bits run the
 // half-size workgroups, two per CU (kSmallPassThreads).
 inline bool small_pass(int fb) { return fb <= 8; }
-inline unsigned pass_tile_rows(int fb) { return small_pass(fb) ? (unsigned)(kSmallPassThreads * kPassRows) : (unsigned)kTile; }
-unsigned pass_grid(u64 n, int fb) {
+// (i32 rows: 8 rows per thread in the half-size workgroups -- 4096-row tiles
+// of 8-B rows -- so a tile's fixed LDS work and barriers serve as many bytes
+// as an int64 tile's; the 1024-thread variant keeps 4: registers)
+constexpr int kSmallNarrowRows = 8;
+inline unsigned pass_tile_rows(int fb, bool wide = true) {
+    if (!small_pass(fb)) return (unsigned)kTile;
+    return (unsigned)(kSmallPassThreads * (wide ? kPassRows : kSmallNarrowRows));
+}
+unsigned pass_grid(u64 n, int fb, bool wide = true) {
     if (!small_pass(fb)) return pass_grid(n);
-    const u64 tiles = (n + pass_tile_rows(fb) - 1) / pass_tile_rows(fb);
+    const u64 tiles = (n + pass_tile_rows(fb, wide) - 1) / pass_tile_rows(fb, wide);
     const u64 g = tiles / 8 > 0 ? tiles / 8 : 1;
     const u64 w = 2ull * (u64)cu_count();
     return (unsigned)(g < w ? g : w);
@@ -2906,7 +2957,7 @@ RadixPlan radix_plan(long long n_build, int force_bits, bool wide) {
     pl.passes = (bits + 8) / 9;   // <= 9 bits (512-way fan-out) per pass
     int left = bits;
     for (int i = 0; i < pl.passes; ++i) {
-        pl.bits[i] = (left + (pl.passes - i) - 1) / (pl.passes - i);
+        pl.bits[i] = (left + (pl.passes - i) - 1) / (pl.passes - i);   // (the larger fan-out first: r04g)
         left -= pl.bits[i];
         pl.pbl[i] = i == pl.passes - 1 ? kFinalPbl : kPassPbl;
     }
@@ -3078,12 +3129,25 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
                         int nseg, const RadixWork &ws, const BucketSet &out, hipStream_t st) {
     int shift = 64 - pl.skip;
     for (int pass = 0; pass < first; ++pass) shift -= pl.bits[pass];
+    // a pass's run placement waits for the next pass's plan and shares its
+    // launch (k_place_plan): both only need the pass's scanned run starts
+    bool pending = false;
+    PlaceArgs pa_prev{};
+    unsigned np_prev = 0;
+    auto place_alone = [&]() {
+        if (pending) hipLaunchKernelGGL(k_bplace, dim3(np_prev), dim3(1024), 0, st, pa_prev);
+        pending = false;
+    };
     for (int pass = first; pass < pl.passes; ++pass) {
         const int fb = pl.bits[pass];
-        const unsigned grid = pass_grid(n > 0 ? n : 1, fb);
+        const unsigned grid = pass_grid(n > 0 ? n : 1, fb, wide);
         const bool small = small_pass(fb);
         shift -= fb;
         const BucketSet &dst = ((pl.passes - 1 - pass) % 2) == 0 ? out : ws.tmp;
+        // bucket-count word and placement cursors by pass parity (the plan of
+        // pass + 1 zeroes its own while pass's placement still uses these)
+        unsigned *nbw = ws.nb + (pass & 1);
+        u64 *rcur = (pass & 1) ? ws.pcur : ws.rcur;
         PassArgs a;
         a.in = src;
         a.n = n;
@@ -3099,7 +3163,7 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         a.out_rows = dst.rows;
         a.bbin = dst.bbin;
         a.bfill = dst.bfill;
-        a.nb = ws.nb;
+        a.nb = nbw;
         {
             // a write past either array is impossible by the capacity bound
             // (radix_need); the kernel still clamps to this
@@ -3109,25 +3173,29 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         a.out_pbl = pl.pbl[pass];
         a.shift = shift;
         a.fbits = fb;
-        a.tile_rows = pass_tile_rows(fb);
-        hipError_t e = hipSuccess;
+        a.tile_rows = pass_tile_rows(fb, wide);
         a.wstart = ws.wstart;
         // the pass counts its buckets' runs per partition into dst.rstart;
-        // the plan kernel zeroes them and k_bplace's cursors first
+        // the plan kernel zeroes them and the placement cursors first
         const u64 P = (u64)nseg << fb;
         a.rcnt = n > 0 ? dst.rstart : nullptr;
         if (grid > 1023) return hipErrorInvalidValue;   // plans: one thread per workgroup + 1
         const unsigned zgrid = blocks_for(P + 1, 1024);
         if (prev && nseg <= kPlanSegs) {
-            // tile map, descriptors, id ranges and zeroing in one launch
+            // tile map, descriptors, id ranges and zeroing in one launch,
+            // with the previous pass's placement when one is pending
             const u64 tb = radix_tiles((long long)n, nseg);
             a.tdesc = (const TileDesc *)ws.tdesc;
             unsigned pg = blocks_for(tb, 1024);
             if (pg < zgrid) pg = zgrid;
             if (pg > 1024) pg = 1024;
-            hipLaunchKernelGGL(k_tile_plan, dim3(pg), dim3(1024), 0, st, a, (const u64 *)prev->rstart, grid, (unsigned)tb,
-                               ws.tile_start, (TileDesc *)ws.tdesc, ws.wstart, dst.rstart, ws.rcur, P + 1);
+            TilePlanArgs tp{a, (const u64 *)prev->rstart, grid, (unsigned)tb, ws.tile_start, (TileDesc *)ws.tdesc,
+                            ws.wstart, dst.rstart, rcur, P + 1};
+            if (pending) hipLaunchKernelGGL(k_place_plan, dim3(np_prev + pg), dim3(1024), 0, st, pa_prev, np_prev, tp);
+            else hipLaunchKernelGGL(k_tile_plan, dim3(pg), dim3(1024), 0, st, tp);
+            pending = false;
         } else {
+            place_alone();
             if (prev) {
                 // tiles of kTile / 64 runs per segment, tile -> segment, and one
                 // descriptor per tile
@@ -3141,14 +3209,15 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
                 a.tdesc = (const TileDesc *)ws.tdesc;
             }
             hipLaunchKernelGGL(k_id_plan, dim3(zgrid < 1024 ? zgrid : 1024), dim3(1024), 0, st, a, prev != nullptr, grid,
-                               ws.wstart, dst.rstart, ws.rcur, P + 1);
+                               ws.wstart, dst.rstart, rcur, P + 1);
         }
         if (n > 0) {
 #define HJ_PASS(W, FORM)                                                                                    \
     do {                                                                                                    \
         if (small)                                                                                          \
-            hipLaunchKernelGGL((k_pass<W, FORM, 0, false, kSmallPassThreads, kSmallFan>), dim3(grid),       \
-                               dim3(kSmallPassThreads), 0, st, a);                                          \
+            hipLaunchKernelGGL((k_pass<W, FORM, 0, false, kSmallPassThreads, kSmallFan,                     \
+                                       W ? kPassRows : kSmallNarrowRows>),                                  \
+                               dim3(grid), dim3(kSmallPassThreads), 0, st, a);                              \
         else hipLaunchKernelGGL((k_pass<W, FORM>), dim3(grid), dim3(kPassThreads), 0, st, a);               \
     } while (0)
             if (prev) {
@@ -3165,17 +3234,18 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         }
         // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
         if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
-        const unsigned lgrid = blocks_for(dst.max_buckets, 1024 * kListPer);
         scan_one(dst.rstart, P + 1, ws, st);
-        hipLaunchKernelGGL(k_bplace, dim3(lgrid), dim3(1024), 0, st, (const unsigned *)dst.bbin,
-                           (const unsigned *)dst.bfill, (const unsigned *)ws.nb, a.max_buckets, pl.pbl[pass],
-                           (const u64 *)dst.rstart, ws.rcur, dst.runs, (int)P);
-        e = hipGetLastError();
+        pa_prev = PlaceArgs{(const unsigned *)dst.bbin, (const unsigned *)dst.bfill, (const unsigned *)nbw, a.max_buckets,
+                            pl.pbl[pass], (const u64 *)dst.rstart, rcur, dst.runs, (int)P};
+        np_prev = blocks_for(dst.max_buckets, 1024 * kListPer);
+        pending = true;
+        const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         prev = &dst;
         nseg = (int)P;
     }
-    return hipSuccess;
+    place_alone();
+    return hipGetLastError();
 }
 
 // Routed rows as a first-pass bucket set: tuples hold, for each source in
