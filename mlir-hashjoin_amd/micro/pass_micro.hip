@@ -1,4 +1,5 @@
 // pass_micro.hip -- ablation of the partition pass kernel (k_pass) on 2^28
+// (round 4: the product's 1024-thread variant; the ABL knobs still apply)
 // packed 16-B rows, first pass (512 bins) and a 256-bin pass.
 // (The ablation of the earlier kernel is kept in
 // profiles/r01_micro_pass_ablation.txt; micro/ws_micro.hip isolates the
@@ -86,13 +87,13 @@ int main(int argc, char **argv) {
             char nm[64];
             snprintf(nm, sizeof nm, "F%d PB%d k_pass", 1 << fb, 1 << pbl);
             run(nm, [&] {
-                hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);
+                hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);
                 hipLaunchKernelGGL((k_pass<true, kPackedRow>), dim3(grid), dim3(kPassThreads), 0, 0, a);
             });
 #define P(ABL, TXT)                                                                                       \
     snprintf(nm, sizeof nm, "F%d PB%d %s", 1 << fb, 1 << pbl, TXT);                                       \
     run(nm, [&] {                                                                                          \
-        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);                    \
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);                    \
         hipLaunchKernelGGL((k_pass<true, kPackedRow, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a);     \
     })
             P(2, "synthetic rows");
@@ -104,7 +105,7 @@ int main(int argc, char **argv) {
             CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
             CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
             a.prof = prof;
-            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst);
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, a, false, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);
             hipLaunchKernelGGL((k_pass<true, kPackedRow, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, a);
             CK(hipDeviceSynchronize());
             std::vector<u64> h(grid * 8);
@@ -154,6 +155,8 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&ws.tdesc, radix_tiles((long long)n, P2) * 16));
         CK(hipMalloc(&ws.wstart, 1025 * 4));
         CK(hipMalloc(&ws.scan_sums, (P2 / 8192 + 2) * 8));
+        CK(hipMalloc(&ws.scan_state, (P2 / 1024 + 4) * 8));   // (one-launch scans: zero between calls)
+        CK(hipMemset(ws.scan_state, 0, (P2 / 1024 + 4) * 8));
         SrcDev src{};
         src.form = kPacked64;
         src.key = in;
@@ -165,7 +168,7 @@ int main(int argc, char **argv) {
             const u64 tb = radix_tiles((long long)n, P1);
             hipLaunchKernelGGL(k_tile_desc, dim3(blocks_for(tb, 256)), dim3(256), 0, 0, (const unsigned *)ws.tile_start,
                                (const unsigned *)ws.tile_owner, (const u64 *)b1.rstart, P1, (unsigned)tb,
-                               (TileDesc *)ws.tdesc);
+                               (TileDesc *)ws.tdesc, (unsigned)(kTile >> kRunLog));
         }
         CK(hipDeviceSynchronize());
         unsigned ntiles = 0;
@@ -195,7 +198,7 @@ int main(int argc, char **argv) {
         b.shift = 64 - 17;
         {
             // correctness: every row must land in the pass-2 output exactly once
-            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);
             hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b);
             CK(hipDeviceSynchronize());
             unsigned nbh = 0;
@@ -217,13 +220,13 @@ int main(int argc, char **argv) {
                    nbh, used, rows, n, rows == n ? "ok" : "MISMATCH", druns, nruns);
         }
         auto p2 = [&] {
-            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
+            hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);
             hipLaunchKernelGGL((k_pass<true, kBucketed>), dim3(grid), dim3(kPassThreads), 0, 0, b);
         };
         run("pass 2 (F256 PB256, runs) k_pass", p2);
 #define P2X(ABL, TXT)                                                                                  \
     run("pass 2 " TXT, [&] {                                                                             \
-        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);                    \
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);                    \
         hipLaunchKernelGGL((k_pass<true, kBucketed, ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b);     \
     })
         P2X(2, "synthetic rows");
@@ -237,7 +240,7 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));
         CK(hipMemset(prof, 0, grid * 8 * sizeof(u64)));
         b.prof = prof;
-        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst);
+        hipLaunchKernelGGL(k_id_plan, dim3(1), dim3(1024), 0, 0, b, true, grid, wst, (u64 *)nullptr, (u64 *)nullptr, 0ull);
         hipLaunchKernelGGL((k_pass<true, kBucketed, PHASE_ABL>), dim3(grid), dim3(kPassThreads), 0, 0, b);
         CK(hipDeviceSynchronize());
         std::vector<u64> h(grid * 8);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round-4: GPU suite, a C3 kernel trace, then SQ counters of given configs
+#   tools/r04_sq.sh <tag> <config> ...
+set -o pipefail
+TAG=$1; shift
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out/$TAG
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > gpurun_out/$TAG/gputest.log 2>&1; rc=$?
+tail -3 gpurun_out/$TAG/gputest.log
+[ $rc -ne 0 ] && exit $rc
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$TAG/trace -o run -- \
+    python3 $R/bench.py --config C3 --no-cpu-baseline --no-host-leg --steps 5 --warmup 2 > $R/gpurun_out/$TAG/trace.log 2>&1 || { echo trace failed; exit 1; }
+for C in "$@"; do
+  bash $R/profiles/collect_sq.sh ${TAG}_$C --config $C || { echo "sq $C failed"; exit 1; }
+done
+echo all done
