@@ -2830,7 +2830,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
 //     build-time sample found repeated build keys (its counting walks lose to
 //     k_join_u's per-row walks there: C1-ref);
 //   int64 rows, probe side >= 8x the build side: k_join_u's stream shape;
-//   i32 rows: k_join_u (fast shape), its deferrals to k_join_grp, or
+//   i32 rows: k_join_b (narrow shape), its deferrals to k_join_grp, or
 //     k_join_grp over every item when the sample says most build keys repeat
 //     (the reference's 10M x 10M keys in [1, 100k]);
 //   whatever those defer: k_join (list mode).
@@ -2859,7 +2859,11 @@ constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 
 // micro/ only): k_join_u over 8192 slots 1.16 ms; k_join_b over 4096 slots
 // 768 x 3+3 0.92, 512 x 5+4 at 3 per CU 0.96, 512 x 5+3 at 4 per CU 1.35 and
 // 1024 x 3+3 1.12 (both spill at the 64-VGPR cap); over 8192 slots 768 x 3+3
-// 0.886, 768 x 4+4 0.779 (this shape); 4+6 and 5+5 spill.
+// 0.886, 768 x 4+4 0.779 (this shape); 4+6 and 5+5 spill.  Round 4: 72 %
+// of REF-B's partitions hold more than this shape's 48 runs per build round
+// (micro/runs_micro.hip), so shapes with larger rounds were tried
+// (profiles/r04_narrow_rounds.txt): 640 x 5+5 at 5 waves per SIMD 1.31 ms,
+// 640 x 6+6 1.24, 896 x 4+4 at 7 per SIMD 1.08, against 0.82 for this one.
 constexpr int kNarrowNT = 768, kNarrowRI = 4, kNarrowSI = 4, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
               kPlanLogNarrow = 13;
 
