@@ -255,8 +255,8 @@ int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
     sb.max_buckets = (unsigned)(cap < 0xFFFFFFF0ull ? cap : 0xFFFFFFF0ull);
     sb.max_rows = sb.rows.bytes / esz;
     // a bucket of f rows lists ceil(f / 64) runs: <= rows / 64 + buckets
-    HJ_TRY(ensure_buf(sb.runs, (size_t)((sb.max_rows >> hj::kRunLog) + sb.max_buckets) * 8));
-    sb.max_runs = sb.runs.bytes / 8;
+    HJ_TRY(ensure_buf(sb.runs, (size_t)((sb.max_rows >> hj::kRunLog) + sb.max_buckets + hj::kRunPad) * 8));
+    sb.max_runs = sb.runs.bytes / 8 - hj::kRunPad;
     return HJ_OK;
 }
 

@@ -140,11 +140,14 @@ struct RadixPlan {
 // runs[rstart[p] .. rstart[p+1]).  Consumers map one wave to one run, so a
 // partly filled bucket idles at most one wave's tail.
 constexpr int kRunLog = 6;
+// readable entries past max_runs in a run list: the joins load a wave's
+// entries in one scalar load of up to 4, past the list's end included
+constexpr int kRunPad = 8;
 constexpr int kFinalPbl = 9;   // 512-row buckets for the join's input (8 / 9 / 10+9 measured: profiles/r01_bucket_sizes.txt)
 struct BucketSet {
     void *rows;                    // >= max_buckets << pbl rows
     unsigned *bbin, *bfill;        // >= max_buckets
-    unsigned long long *runs;      // >= max_runs
+    unsigned long long *runs;      // >= max_runs + kRunPad (readable)
     unsigned long long *rstart;    // >= P + 1 (P of the pass writing the set)
     unsigned max_buckets;          // bbin / bfill entries
     unsigned long long max_rows;   // rows entries

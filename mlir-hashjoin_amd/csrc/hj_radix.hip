@@ -785,7 +785,26 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
         }
         __syncthreads();
         mark(2);
-        {
+        if constexpr (!WIDE && !EXACT) {
+            // 8-B rows: two rows per lane, one 16-B store (L / 2 lanes per
+            // line, 128 / L lines per store instruction): REF-B's passes
+            // 0.80 -> 0.74 ms each (16-B loads of two rows per lane were
+            // tried with it and lost that again: profiles/r04_join_entries.txt)
+            constexpr unsigned LH = L / 2, LPW2 = 64u / LH;
+            const unsigned nl = s_nl, g = (threadIdx.x & 63u) / LH, r2 = (threadIdx.x & (LH - 1)) * 2u;
+            for (unsigned l0 = wave * LPW2; l0 < nl; l0 += (unsigned)(kPassThreads / 64) * LPW2) {
+                const unsigned x = l0 + g;
+                if (x >= nl) continue;
+                const unsigned b = lbin[x];
+                const unsigned f = fill[b], tl0 = f & (L - 1);
+                const unsigned off = (x - lstart[b]) * L + r2;
+                const unsigned p = f - tl0 + off;
+                const T v0 = off < tl0 ? tail[b * (L - 1) + off] : stage[start[b] + (off - tl0)];
+                const T v1 = off + 1 < tl0 ? tail[b * (L - 1) + off + 1] : stage[start[b] + (off + 1 - tl0)];
+                const u64 o = slot(b, p);
+                if ((ABL & 4) == 0 && o != ~0ull) st_s<kNtPassSt>((ulonglong2 *)(out + o), make_ulonglong2(v0, v1));
+            }
+        } else {
             // complete lines: L lanes per line, 64 / L lines per store
             // instruction; a line's rows are the bin's old tail rows, then
             // its staged new rows
@@ -2210,15 +2229,33 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
     const unsigned off = threadIdx.x & ((1u << kRunLog) - 1u);
     const int lane = threadIdx.x & 63;
     const u64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) {
+    // i32 rows: the wave's n consecutive entries [lo + wv0 * n, + n) as they
+    // are (adjacent scalar loads, merged into one: strided conditional ones
+    // each waited for the one before; a list has kRunPad readable entries
+    // past any hi); returns how many are the list's -- rows_of drops the
+    // others, so no instruction uses a loaded word before the rows are wanted
+    auto ents = [&](const u64 *list, u64 lo, u64 hi, u64 *e, int n) -> unsigned {
+        if constexpr (WIDE) {
+            // entries lo + i * NW + wv0 (the wide shape measured 1-3 % slower
+            // with the narrow one's contiguous entries: profiles/r04_join_entries.txt)
 #pragma unroll
-        for (int i = 0; i < n; ++i) {
-            const u64 li = lo + (u64)i * NW + wv0;
-            e[i] = li < hi ? sload(list + li) : 0ull;
+            for (int i = 0; i < n; ++i) {
+                const u64 li = lo + (u64)i * NW + wv0;
+                e[i] = li < hi ? sload(list + li) : 0ull;
+            }
+            return (unsigned)n;
         }
+        const u64 b0 = lo + (u64)wv0 * n;
+        const u64 bl = b0 < hi ? b0 : 0ull;
+#pragma unroll
+        for (int i = 0; i < n; ++i) e[i] = sload(list + bl + i);
+        return b0 < hi ? (hi - b0 < (u64)n ? (unsigned)(hi - b0) : (unsigned)n) : 0u;
     };
-    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
+    auto rows_of = [&](const T *rows, const u64 *e0, unsigned nv, T *v, int n) {
         unsigned ok = 0;
+        u64 e[RI > SI ? RI : SI];
+#pragma unroll
+        for (int i = 0; i < n; ++i) e[i] = (unsigned)i < nv ? e0[i] : 0ull;
 #pragma unroll
         for (int i = 0; i < n; ++i) {
             const bool in = off < (unsigned)(e[i] & 127u);
@@ -2252,9 +2289,9 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
     T sv_[SI], rv_[RI];
     u64 er[RI], es[SI];
     ItemDesc it = sload(a.desc + w);
-    ents(a.r_runs, it.r_lo, it.r_hi, er, RI);
+    unsigned nvr = ents(a.r_runs, it.r_lo, it.r_hi, er, RI), nvs = 0;
     // (DETECT reads no probe rows)
-    if (!DETECT) ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
+    if (!DETECT) nvs = ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
     constexpr bool dyn = !DETECT && !WIDE;
     if (dyn) {
         if (threadIdx.x == 0) s_next = w + gridDim.x;
@@ -2264,17 +2301,18 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
         const bool fits = it.r_hi - it.r_lo <= (u64)rmax;
         unsigned rok = 0, sok = 0;
         if (fits) {
-            rok = rows_of(rrows, er, rv_, RI);
-            if (!DETECT) sok = rows_of(srows, es, sv_, SI);
+            rok = rows_of(rrows, er, nvr, rv_, RI);
+            if (!DETECT) sok = rows_of(srows, es, nvs, sv_, SI);
         }
         const unsigned wn = dyn ? __builtin_amdgcn_readfirstlane(s_next) : w + gridDim.x;
         const bool more = wn < total;
         u64 ner[RI], nes[SI];
+        unsigned nnvr = 0, nnvs = 0;
         ItemDesc nx = it;
         if (more) {
             nx = sload(a.desc + wn);
-            ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
-            if (!DETECT) ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
+            nnvr = ents(a.r_runs, nx.r_lo, nx.r_hi, ner, RI);
+            if (!DETECT) nnvs = ents(a.s_runs, nx.s_lo, nx.s_lo + subb < nx.s_hi ? nx.s_lo + subb : nx.s_hi, nes, SI);
         }
         if (!fits) {
             // (DETECT: to k_join's list-mode build, which flags repeats)
@@ -2363,8 +2401,8 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                 }
                 r0 += rb;
                 if (r0 >= it.r_hi) break;
-                ents(a.r_runs, r0, it.r_hi, er, RI);
-                rok = rows_of(rrows, er, rv_, RI);
+                nvr = ents(a.r_runs, r0, it.r_hi, er, RI);
+                rok = rows_of(rrows, er, nvr, rv_, RI);
             }
             if (bad) s_bad = 1u;
             __syncthreads();
@@ -2439,8 +2477,8 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
             };
                 for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
                     if (sb != it.s_lo) {
-                        ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
-                        sok = rows_of(srows, es, sv_, SI);
+                        nvs = ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
+                        sok = rows_of(srows, es, nvs, sv_, SI);
                     }
                     unsigned pm = 0u;
 #pragma unroll
@@ -2590,8 +2628,11 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
         // (plain loops: with DETECT's unused S entries the unroll pragma
         // could not be honoured for its instantiation and warned)
         for (int i = 0; i < RI; ++i) er[i] = ner[i];
-        if constexpr (!DETECT)
+        nvr = nnvr;
+        if constexpr (!DETECT) {
             for (int i = 0; i < SI; ++i) es[i] = nes[i];
+            nvs = nnvs;
+        }
     }
 }
 
