@@ -229,3 +229,23 @@ def test_c4_eight_owner_folded_2p28(hj):
     del outs
     assert bool((rk[o_r] == sk[o_s]).all())
     assert torch.equal(torch.sort(o_s)[0], torch.arange(n, device="cuda"))
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_folded_duplicates_after_parts(hj, oracle, dups):
+    """has_duplicates() after a routed build probed in 2 bin ranges: the
+    repeat check covers the whole routed build side, not only the bins the
+    last hj_dev_probe_routed_i64 call joined.  The repeated key
+    is one no probe row meets."""
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(91, 40000, 30000, 0.9)
+    if dups:
+        rk = rk.copy()
+        rk[-1] = rk[-2]
+        keep = sk != rk[-2]
+        sk, sp = sk[keep], sp[keep]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    outs = _owner_join_folded(hj, d(rk), d(rp), d(sk), d(sp), 1, 5, s_parts=2)
+    got_r = np.concatenate([o[0].cpu().numpy() for o in outs])
+    got_s = np.concatenate([o[1].cpu().numpy() for o in outs])
+    assert oracle.same_multiset(got_r, got_s, *oracle.nested_loop_i64(rk, rp, sk, sp))
+    assert hj.has_duplicates() == dups

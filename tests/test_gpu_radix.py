@@ -580,3 +580,29 @@ def test_radix_fuzz_ragged_vs_oracle(hj, oracle, i, nr, ns, span, bits, wide):
         finally:
             hj.set_strategy("auto")
         assert oracle.same_multiset(g_r.cpu().numpy().astype(np.int64), g_s.cpu().numpy().astype(np.int64), *exp)
+
+
+@pytest.mark.parametrize("wide", [True, False])
+@pytest.mark.parametrize("dups", [False, True])
+def test_radix_duplicates_in_unprobed_partitions(hj, oracle, wide, dups):
+    """has_duplicates() after a join whose probe side reaches only a handful
+    of the 4096 build partitions: the on-demand check (radix_detect) covers
+    the whole build side, so a repeated build key in a partition no probe row
+    reached is still reported, and unique keys are not."""
+    n = 200000
+    rng = np.random.default_rng(4242 + (1 if wide else 0))
+    rk = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
+    sk = rk[:8].copy()   # 8 probe rows: at most 8 of the 4096 partitions probed
+    if dups:
+        rk[n - 1] = rk[n - 2]   # (neither key is probed)
+    rp = np.arange(n, dtype=np.int64) * 7 + 3
+    sp = np.arange(len(sk), dtype=np.int64) + 11
+    if wide:
+        o = run(hj, rk, rp, sk, sp, 12)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
+    else:
+        o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 12)
+        ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
+        assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
+    assert len(o[0]) == 8
+    assert hj.has_duplicates() == dups
