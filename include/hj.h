@@ -102,7 +102,9 @@ int hj_ctx_radix_plan(const hj_ctx *ctx, int *passes, int bits[3]);
 /* 1 if the build side repeats a key, 0 if not (synchronises).  Known after
  * the build (GLOBAL) or after the first probe (RADIX: a repeat that a probe
  * row met is flagged by the join; the first call after a join whose kernel
- * was k_join_b checks the rest of its build partitions on the device). */
+ * was k_join_b checks every partition of the build side on the device,
+ * including those no probe row reached and, after routed probes in several
+ * bin ranges, every range). */
 int hj_ctx_build_has_duplicates(hj_ctx *ctx);
 /* Per-phase kernel timing with HIP events on the caller's stream. */
 int hj_ctx_set_timing(hj_ctx *ctx, int enable);

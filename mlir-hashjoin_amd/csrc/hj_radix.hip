@@ -452,16 +452,6 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
     constexpr int kLines = (kTile + kMaxFan * (L - 1)) / L;
     __shared__ unsigned short lbin[kLines];
     __shared__ unsigned s_nl;
-    // bins with more than kLbinOwn complete lines in the tile: their owner
-    // thread maps the first kLbinOwn, the whole workgroup the rest (a skewed
-    // bin's 256 lines were one thread's serial loop, ~3.5k cycles per tile
-    // of C4's hot segment: micro/skew_micro.hip)
-    // (not in the 9-bit int64 bucketed pass: its VGPRs are at the 4-waves
-    // cap, and it spilled 16 B)
-    constexpr bool BIGMAP = !(WIDE && FORM == kBucketed && FMAX > 256);
-    constexpr unsigned kLbinOwn = BIGMAP ? 8u : ~0u;
-    __shared__ unsigned short s_big[BIGMAP ? kLines / 8 + 1 : 1];
-    __shared__ unsigned s_nbig, s_anybig;
     // EXACT: out row of bin b's position 0 (the slot base rounded down to a
     // line; positions below cur[b] belong to the slot before)
     __shared__ u64 cbase[EXACT ? kMaxFan : 1];
@@ -722,7 +712,6 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
             // 0 alone is on the critical path here)
             constexpr int BPL = FMAX / 64, Q = BPL / 4;
             unsigned c[BPL], k[BPL], ln[BPL], s = 0, sk = 0, sl = 0;
-            bool big = false;   // (any of this lane's bins has more than kLbinOwn lines)
 #pragma unroll
             for (int qd = 0; qd < Q; ++qd) {
                 const uint4 c4 = ((const uint4 *)cnt)[lane * Q + qd];
@@ -736,7 +725,6 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
                     k[j] = (!EXACT && c[j]) ? (fv[jj] + c[j] - 1) >> a.out_pbl : 0u;
                     // complete lines: the old tail's and the new rows'
                     ln[j] = c[j] ? ((fv[jj] & (L - 1)) + c[j]) / L : 0u;
-                    if constexpr (BIGMAP) big |= ln[j] > kLbinOwn;
                     s += c[j];
                     sk += k[j];
                     sl += ln[j];
@@ -753,7 +741,6 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
                 if (lane == 0) s_hot = (mx >> 16) > (unsigned)(kTile / 8) ? (mx & 0xffffu) : 0xFFFFFFFFu;
             }
             const unsigned x = wave_incl_add(s), xk = wave_incl_add(sk), xl = wave_incl_add(sl);
-            const bool anybig = BIGMAP && __ballot(big) != 0ull;
             unsigned run = x - s, runk = xk - sk, runl = xl - sl;
             unsigned sv[BPL], nv[BPL], lv[BPL];
 #pragma unroll
@@ -775,8 +762,6 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
             }
             if (lane == 63) {
                 s_nl = xl;
-                s_anybig = anybig ? 1u : 0u;
-                s_nbig = 0u;   // (the previous tile's readers are past two barriers)
                 s_nb = id_next;
                 s_nend = id_end;
                 id_next = xk < id_end - id_next ? id_next + xk : id_end;
@@ -799,21 +784,21 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
             else stage[start[b] + rk] = row[i];
         }
         // the line -> bin map (a bin owner per thread)
+        // (this tile's largest bin, when it holds more than kTile / 8 rows
+        // -- s_hot, set by the scan for the next tile's count -- is mapped by
+        // the whole workgroup: one thread's serial loop over a skewed bin's
+        // 256 lines cost ~3.5k cycles per tile of C4's hot segment,
+        // micro/skew_micro.hip)
+        const unsigned hot = s_hot;
         for (unsigned b = threadIdx.x; b < F; b += kPassThreads) {
             const unsigned c = cnt[b];
-            if (!c) continue;
+            if (!c || b == hot) continue;
             const unsigned nl = ((fill[b] & (L - 1)) + c) / L, l0 = lstart[b];
-            const unsigned own = nl < kLbinOwn ? nl : kLbinOwn;
-            for (unsigned x = 0; x < own; ++x) lbin[l0 + x] = (unsigned short)b;
-            if (BIGMAP && nl > kLbinOwn) s_big[atomicAdd(&s_nbig, 1u)] = (unsigned short)b;
+            for (unsigned x = 0; x < nl; ++x) lbin[l0 + x] = (unsigned short)b;
         }
-        if (BIGMAP && s_anybig) {   // (uniform; only tiles with a skewed bin pay the barrier)
-            __syncthreads();
-            for (unsigned q = 0; q < s_nbig; ++q) {
-                const unsigned b = s_big[q];
-                const unsigned nl = ((fill[b] & (L - 1)) + cnt[b]) / L, l0 = lstart[b];
-                for (unsigned x = kLbinOwn + threadIdx.x; x < nl; x += kPassThreads) lbin[l0 + x] = (unsigned short)b;
-            }
+        if (hot != 0xFFFFFFFFu) {   // (uniform)
+            const unsigned nl = ((fill[hot] & (L - 1)) + cnt[hot]) / L, l0 = lstart[hot];
+            for (unsigned x = threadIdx.x; x < nl; x += kPassThreads) lbin[l0 + x] = (unsigned short)hot;
         }
         __syncthreads();
         mark(2);
