@@ -74,3 +74,25 @@ def test_routing_balance_under_skew():
     c = counts.cpu().numpy().astype(float)
     assert c.sum() == n and c.max() / c.mean() < 1.25
     hj.close()
+
+
+@pytest.mark.parametrize("hot_frac", [0.3, 0.9])
+def test_radix_heavy_hot_key_2p22(hj, hot_frac):
+    """One key carrying 30 % / 90 % of the probe side through a 2-pass radix
+    plan: the partition passes' hot-bin paths (one LDS add per wave for the
+    hot rows, the hot bin's lines mapped by the whole workgroup) and the
+    join's long items.  PK-FK, so every probe row matches exactly once:
+    every pair is a true match and every S row appears once."""
+    n = 1 << 22
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0xC4 + int(hot_frac * 10), n, n)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    hot = torch.rand(n, device="cuda", generator=g) < hot_frac
+    sk = torch.where(hot, rk[12345], sk)
+    hj.set_strategy("radix")
+    o_r, o_s = hj.join(rk, rp, sk, sp)
+    hj.set_strategy("auto")
+    assert len(hj.radix_plan) >= 2
+    assert o_r.numel() == n
+    # (payloads are row ids: R.pay = R row, S.pay = S row)
+    assert bool((rk[o_r] == sk[o_s]).all())
+    assert torch.equal(torch.sort(o_s)[0], torch.arange(n, device="cuda"))
