@@ -119,7 +119,9 @@ __device__ __forceinline__ void st_s(T *p, const T &v) {
         __builtin_nontemporal_store(v, p);
     }
 }
-constexpr bool kNtPassLd = false, kNtPassSt = true;
+// (nt loads in the passes: 1 % off C3's step since the stores are whole nt
+// lines; with plain stores they lost 0.3 ms -- profiles/r04_pass_nt_loads.txt)
+constexpr bool kNtPassLd = true, kNtPassSt = true;
 constexpr bool kNtJoinLd = true, kNtJoinSt = true;
 
 // Row `row` of a pass input in form FORM.
