@@ -66,6 +66,67 @@ PROBE_KERNELS = ("k_pass",)
 FAST_JOIN_KERNELS = ("k_join_b", "k_join_u", "k_join_grp")
 OPTIONAL_PROBE_KERNELS = FAST_JOIN_KERNELS + ("k_join",)
 
+# roofline scopes.  t_probe always contains EVERY partition
+# pass of S: on the distributed path S's first pass runs inside its routing
+# (the EXACT k_pass), so the t_probe figure there adds S's route time; the
+# local-only figure is reported beside it under its own name.
+SCOPE_T_PROBE = "probe phase: S radix partition passes + the LDS join (SURVEY 8(d) t_probe)"
+SCOPE_T_PROBE_DIST = ("probe phase incl. S's routing (SURVEY 8(d) t_probe, every S partition pass): S's route "
+                      "(k_slot_hist + EXACT k_pass + count exchange) + S's local k_pass + the LDS join")
+SCOPE_LOCAL_PROBE = ("local probe only, NOT t_probe: S's local (second) k_pass + the LDS join; S's first "
+                     "partition pass ran in the route phase")
+SCOPE_GLOBAL = "probe phase: k_probe + k_probe_slow (global table)"
+COPY_FLOOR_ROWS = 1 << 28   # 16-B rows: 4 GiB read + 4 GiB written = one C3 partition pass's bytes
+
+
+def frac_of(b, t_ms, peak=HBM_PEAK_GBS):
+    return round(b / (t_ms / 1000.0) / 1e9 / peak, 4) if t_ms and t_ms > 0 else None
+
+
+def probe_roofline(strategy, use_dist, probe_ms, s_route_ms, probe_bytes, read_bytes, structure_bytes=None,
+                   floor=None):
+    """The probe-phase roofline record.  probe_ms: the probe
+    phase's HIP-event time; s_route_ms: S's routing on the distributed path
+    (0 otherwise); structure_bytes: the phase's structural HBM bytes (every
+    S pass + the join), priced at the box's own copy rates from `floor`."""
+    dist_t = bool(use_dist and s_route_ms)
+    t = probe_ms + (s_route_ms if dist_t else 0.0)
+    if strategy != "radix":
+        scope = SCOPE_GLOBAL
+    else:
+        scope = SCOPE_T_PROBE_DIST if dist_t else SCOPE_T_PROBE
+    roof = {
+        "scope": scope,
+        "bound": "hbm",
+        "achieved": round(probe_bytes / (t / 1000.0) / 1e9, 1) if t > 0 else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": frac_of(probe_bytes, t),
+        "algorithmic_bytes": probe_bytes,
+        "ms": round(t, 4),
+        "frac_of_achievable": frac_of(probe_bytes, t, HBM_ACHIEVABLE_GBS),
+        # north_star's "HBM read roofline": the probe phase's algorithmic READ
+        # bytes only (S row + one slot per probe tuple; SURVEY 8(d))
+        "read_bytes": read_bytes,
+        "read_frac": frac_of(read_bytes, t),
+        "target": "north_star: frac >= 0.40 at |R|=|S|=2^28 (t_probe <= 4.0 ms)",
+    }
+    if dist_t:
+        roof["s_route_ms"] = round(s_route_ms, 4)
+        roof["local_probe"] = {"scope": SCOPE_LOCAL_PROBE, "ms": round(probe_ms, 4),
+                               "frac": frac_of(probe_bytes, probe_ms)}
+    if floor and structure_bytes and strategy == "radix":
+        fl = structure_bytes / (floor["persistent_gbs"] * 1e6)
+        ff = structure_bytes / (floor["flat_gbs"] * 1e6)
+        roof["structure_bytes"] = int(structure_bytes)
+        roof["floor_ms"] = round(fl, 4)
+        roof["floor_flat_ms"] = round(ff, 4)
+        roof["phase_over_floor"] = round(t / fl, 4) if fl > 0 else None
+        roof["phase_over_flat_floor"] = round(t / ff, 4) if ff > 0 else None
+        roof["floor_note"] = ("structure_bytes (every S pass + the join's R, S and pairs) at this box's own "
+                              "copy rates, measured in-process before the warm-up (copy_floor)")
+    return roof
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -84,6 +145,7 @@ def parse():
                     help="use the multi-GPU code path (partition + all-to-all) even at N=1")
     ap.add_argument("--s-parts", type=int, default=0,
                     help="multi-GPU path: batches the shuffled probe side moves in (0: hashjoin.dist default)")
+    ap.add_argument("--no-floor", action="store_true", help="skip the in-process copy floor (roofline.floor_ms)")
     ap.add_argument("--log2", type=int, default=0,
                     help="experiments: |R| = |S| = 2^LOG2 rows instead of the config's sizes (not a bench line)")
     return ap.parse_args()
@@ -250,6 +312,40 @@ def traffic_of(rec, names, optional=(), pass_forms=None):
     return int(tot)
 
 
+def copy_floor(hashjoin, reps=5):
+    """This box's streamed-copy rate, measured in-process: 2^28 16-B rows
+    (4 GiB read + 4 GiB written) copied by hj_dev_stream_copy in the radix
+    passes' persistent shape and in the flat one-row-per-thread shape; HIP
+    events on the launching stream, median of `reps`."""
+    rows = COPY_FLOOR_ROWS
+    a = torch.full((2 * rows,), 7, dtype=torch.int64, device="cuda")
+    b = torch.empty_like(a)
+    nbytes = 2 * rows * 16
+    res = {"bytes": nbytes, "reps": reps}
+    for shape in ("persistent", "flat"):
+        hashjoin.stream_copy(a, b, shape)
+        ts = []
+        for _ in range(reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            hashjoin.stream_copy(a, b, shape)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ts.sort()
+        med = ts[len(ts) // 2]
+        res[f"{shape}_ms"] = round(med, 4)
+        res[f"{shape}_gbs"] = round(nbytes / (med / 1000.0) / 1e9, 1)
+    assert bool((b[:4] == 7).all()), "copy floor: destination not written"
+    del a, b
+    torch.cuda.empty_cache()
+    res["shapes"] = ("persistent: one 1024-thread workgroup per CU, contiguous 4096-row tile range, next tile "
+                     "prefetched (the passes' shape); flat: one row per thread, 256-thread workgroups; nt loads "
+                     "and stores")
+    return res
+
+
 # ---------------------------------------------------------------- main
 def gen_inputs(hashjoin, a, NR, NS, distn, r0, nr, s0, ns):
     if distn == "pkfk":
@@ -344,7 +440,8 @@ def main():
     expect_m = expected_rows(distn, NR, NS)
     torch.cuda.synchronize()
 
-    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0, "route": 0.0}
+    phases = {"init": 0.0, "build": 0.0, "probe": 0.0, "probe_partition": 0.0, "probe_join": 0.0, "route": 0.0,
+              "s_route": 0.0}
     last = {}
 
     if not use_dist:
@@ -385,12 +482,17 @@ def main():
                 # transfers overlap compute (hashjoin.dist): R's tuples move
                 # during S's routing, S's during R's build
                 phases["route"] += ev["start"].elapsed_time(ev["routed"])
+                if "s_route" in ev:
+                    phases["s_route"] += ev["s_route"].elapsed_time(ev["routed"])
                 phases["build"] += ev["routed"].elapsed_time(ev["built"])
                 phases["probe"] += ev["built"].elapsed_time(ev["probed"])
             last["m"] = o_r.numel()
             last["rows"] = ev["rows"]
             last["mode"] = ev["mode"] + (", folded routing" if ev.get("folded") else "")
 
+    # the box's own copy rate (outside the timed steps): every line states how
+    # far its probe phase is from it (roofline.floor_ms / phase_over_floor)
+    floor = None if a.no_floor else copy_floor(hashjoin)
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()
@@ -448,33 +550,34 @@ def main():
     rec, traffic_note = pmc_record(a.config + ("-dist" if use_dist else ""), world)
     info = hashjoin.device_info(local)
 
-    def frac(b, t_ms, peak=HBM_PEAK_GBS):
-        return round(b / (t_ms / 1000.0) / 1e9 / peak, 4) if t_ms > 0 else None
-
-    roof = {
-        "scope": ("probe phase: S radix partition passes + the LDS join (SURVEY 8(d) t_probe)" if strategy == "radix"
-                  else "probe phase: k_probe + k_probe_slow (global table)"),
-        "bound": "hbm",
-        "achieved": round(probe_bytes / (probe_ms / 1000.0) / 1e9, 1) if probe_ms > 0 else None,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": frac(probe_bytes, probe_ms),
-        # (the distributed path's probe phase: the routed S's one local pass,
-        # the bucketed-input k_pass, + the join; routing is its own phase)
-        "traffic": (traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS,
-                               pass_forms=("<true, 4,", "<false, 4,") if use_dist else None)
-                    if strategy == "radix" and (not use_dist or world == 1) else None),
-        "traffic_source": traffic_note,
-        "algorithmic_bytes": probe_bytes,
-        "bytes_per_probe_row": round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2),
-        "ms": round(probe_ms, 4),
-        "frac_of_achievable": frac(probe_bytes, probe_ms, HBM_ACHIEVABLE_GBS),
-        # north_star's "HBM read roofline": the probe phase's algorithmic READ
-        # bytes only (S row + one slot per probe tuple)
-        "read_bytes": read_bytes,
-        "read_frac": frac(read_bytes, probe_ms),
-        "target": "north_star: frac >= 0.40 at |R|=|S|=2^28 (t_probe <= 4.0 ms)",
-    }
+    s_route_ms = phases["s_route"] / a.steps
+    # structural HBM bytes of t_probe: every S partition pass + the join
+    W = 16 if wide else 8
+    kbytes_loc = ((last["rows"][0] if use_dist else nr) + (last["rows"][1] if use_dist else ns)) * W + m_local * PAIR
+    ns_probe = last["rows"][1] if use_dist else ns
+    if use_dist and s_route_ms > 0:
+        # S: key histogram (8 B) + EXACT pass (32 B) in the route, one local pass (32 B)
+        structure = ns * (8 + 32) + ns_probe * 32 + kbytes_loc
+    elif wide:
+        structure = ns_probe * 32 * max(1, hj.radix_passes) + kbytes_loc
+    else:
+        structure = ns_probe * (12 + 16 * max(0, hj.radix_passes - 1)) + kbytes_loc
+    roof = probe_roofline(strategy, use_dist, probe_ms, s_route_ms, probe_bytes, read_bytes,
+                          structure_bytes=structure if strategy == "radix" else None, floor=floor)
+    roof["bytes_per_probe_row"] = round(probe_bytes / max(1, ns if not use_dist else last["rows"][1]), 2)
+    if strategy == "radix" and use_dist and world == 1 and "local_probe" in roof:
+        # every S kernel of t_probe: EXACT + local k_pass variants, the key histogram, the join
+        roof["traffic"] = traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS + ("k_slot_hist",))
+        roof["local_probe"]["traffic"] = traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS,
+                                                    pass_forms=("<true, 4,", "<false, 4,"))
+    elif strategy == "radix" and not use_dist:
+        roof["traffic"] = traffic_of(rec, PROBE_KERNELS, OPTIONAL_PROBE_KERNELS)
+    else:
+        roof["traffic"] = None
+    roof["traffic_source"] = traffic_note
+    if floor:
+        roof["copy_floor"] = floor
+    frac = frac_of
     if not use_dist and strategy == "radix":
         kbytes = (nr + ns) * (16 if wide else 8) + m_local * PAIR
         # the kernel is a function of the data (row width, |S| / |R|, the build

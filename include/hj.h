@@ -243,6 +243,21 @@ int hj_dev_select_f32(hj_ctx *ctx, const float *in, int64_t n, int cmp, float va
 int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_t value, int64_t *out,
                       int64_t *out_row, int64_t out_cap, uint64_t *d_count, void *stream);
 
+/* Copy floor (measurement helper, no reference counterpart: SURVEY 8(d)
+ * asks every figure to be set against the box's own HBM rate).  Copies
+ * `rows` 16-B rows from `in` to `out` (device pointers, 16-B aligned) with
+ * non-temporal loads and stores, in one of two shapes:
+ *   HJ_COPY_PERSISTENT: one 1024-thread workgroup per CU over a contiguous
+ *     range of 4096-row tiles, next tile's loads in flight (the radix
+ *     partition passes' loop shape);
+ *   HJ_COPY_FLAT: one row per thread over a grid of 256-thread workgroups
+ *     (the fastest streamed copy this chip runs).
+ * Asynchronous on `stream`; HJ_ERR_ARG for a bad shape or misaligned
+ * pointer. */
+#define HJ_COPY_PERSISTENT 0
+#define HJ_COPY_FLAT 1
+int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void *stream);
+
 /* Out-of-core join of HOST-resident int64 key/payload columns (relations
  * larger than HBM; the reference leaves the partitioned join out,
  * projectDescription.md:23-24).  When R does not fit device_budget bytes

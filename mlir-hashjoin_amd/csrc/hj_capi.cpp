@@ -46,6 +46,17 @@ int fail(int code, const char *file, int line, const std::string &msg) {
         if (e_ != hipSuccess)                                                                     \
             return fail(HJ_ERR_HIP, __FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
+// A radix call that fails may leave the one-launch scan's tile words set
+// (they are zeroed only on allocation, and every completed scan clears
+// them): reset them on the stream before reporting the failure.
+#define HJ_RADIX(ctx, st, expr)                                                                    \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            if ((ctx)->scan_state.p) (void)hipMemsetAsync((ctx)->scan_state.p, 0, (ctx)->scan_state.bytes, (st)); \
+            return fail(HJ_ERR_HIP, __FILE__, __LINE__, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+        }                                                                                          \
+    } while (0)
 #define HJ_TRY(expr)              \
     do {                          \
         int r_ = (expr);          \
@@ -165,6 +176,18 @@ struct hj_ctx {
         int reuse = 0;   // HJ_REUSE_* the count ran under
         // HJ_REUSE_EXACT: the count's inputs, compacted (keys, then payloads)
         std::vector<unsigned char> cr, cs;
+        // drop the memo; the EXACT-mode copies (GBs at 2^28 rows) give
+        // their memory back unless `keep` (a count about to refill them)
+        void invalidate(bool keep = false) {
+            valid = false;
+            if (keep) {
+                cr.clear();
+                cs.clear();
+            } else {
+                std::vector<unsigned char>().swap(cr);
+                std::vector<unsigned char>().swap(cs);
+            }
+        }
     } memo;
     long long memo_hits = 0;
     // the last radix probe's shape, for hj_ctx_join_kernel (the kernel itself
@@ -336,7 +359,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->join_ran = false;
     c->dup_checked = false;
     c->routed = false;
-    c->memo.valid = false;   // (hj_count_*'s kept table is gone)
+    c->memo.invalidate();   // (hj_count_*'s kept table is gone)
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
@@ -350,7 +373,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         HJ_HIP(hipMemsetAsync(c->meta, 0, 4 * sizeof(unsigned long long), st));
         record(c, kEvInit1, st);
         trace("build: workspace", st, src.n);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->rset), st));
+        HJ_RADIX(c, st, hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->rset), st));
         // repeated build keys, sampled: decides the join kernel (radix_join)
         HJ_HIP(hj::radix_sample(wide, c->plan, bucket_set(c->rset), c->meta + 2, st));
         trace("build: R partitioned", st, (long long)c->plan.total_bits);
@@ -391,18 +414,18 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         HJ_TRY(ensure_radix_scratch(c, c->sset, src.n, esz, c->plan));
         trace("probe: workspace", st, (long long)c->sset.max_buckets);
         record(c, kEvProbe0, st);
-        HJ_HIP(hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
+        HJ_RADIX(c, st, hj::radix_partition(src, wide, c->plan, radix_work(c), bucket_set(c->sset), st));
         trace("probe: S partitioned", st, src.n);
         record(c, kEvProbeMid, st);
         // the kernel: a function of (row width, size ratio, build-time sample)
         const bool stream = src.n >= 8 * c->n_build;
-        HJ_HIP(hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
+        HJ_RADIX(c, st, hj::radix_join(wide, c->plan, radix_work(c), bucket_set(c->rset), bucket_set(c->sset), c->sset.max_runs,
                               (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, count_only ? 0 : cap,
                               (unsigned long long *)d_count, c->meta + 1, count_only, st, c->meta + 2, stream));
         c->join_ran = true;
         c->join_wide = wide;
         c->join_stream = stream;
-            trace("probe: joined", st, cap);
+        trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
         c->rec[2] = c->timing;
         c->rec_mid = c->timing;
@@ -845,7 +868,7 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
             return HJ_OK;
         }
     }
-    mm.valid = false;
+    mm.invalidate(mode == kHostCount && reuse == HJ_REUSE_EXACT);
     const size_t rb = (size_t)(layout == kWide ? 16 : 4) * (size_t)r.n;
     const size_t sb = (size_t)(layout == kWide ? 16 : 4) * (size_t)s.n;
     void *dr_buf, *ds_buf;
@@ -854,8 +877,6 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     hj::SrcDev rsrc, ssrc;
     {
         Joiner dig;
-        mm.cr.clear();
-        mm.cs.clear();
         if (mode == kHostCount && reuse == HJ_REUSE_DIGEST) dig.t = std::thread([&] {   // overlapped with the upload
             dr = digest_rel(r, esz);
             ds = digest_rel(s, esz);
@@ -1021,7 +1042,20 @@ int hj_device_info(int device, int64_t out[8]) {
 
 int hj_host_set_reuse(int mode) {
     if (mode != HJ_REUSE_DIGEST && mode != HJ_REUSE_EXACT && mode != HJ_REUSE_OFF) HJ_FAIL(HJ_ERR_ARG, "bad reuse mode");
-    return g_reuse.exchange(mode);
+    const int prev = g_reuse.exchange(mode);
+    if (prev == HJ_REUSE_EXACT && mode != HJ_REUSE_EXACT) {
+        // the EXACT copies can no longer be used: give their memory back
+        std::vector<hj_ctx *> ctxs;
+        {
+            std::lock_guard<std::mutex> lk(g_default_mu);
+            for (auto &kv : g_default) ctxs.push_back(kv.second);
+        }
+        for (hj_ctx *c : ctxs) {
+            std::lock_guard<std::mutex> host_lk(c->host_mu);
+            c->memo.invalidate();
+        }
+    }
+    return prev;
 }
 
 int64_t hj_host_memo_hits(void) {
@@ -1120,8 +1154,9 @@ int hj_ctx_build_has_duplicates(hj_ctx *c) {
         // only those a probe row met): the exact answer, once per build, is a
         // DETECT build over every partition of R (the work map is rebuilt from
         // R alone; the last join's map is not needed again)
-        HJ_HIP(hj::radix_detect(c->layout == kWide, c->plan, radix_work(c), bucket_set(c->rset),
-                                (unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1, c->meta + 2, nullptr));
+        HJ_RADIX(c, nullptr, hj::radix_detect(c->layout == kWide, c->plan, radix_work(c), bucket_set(c->rset),
+                                               (unsigned *)c->work_start.p, c->work_desc.p, c->meta + 1,
+                                               c->meta + 2, nullptr));
         HJ_HIP(hipDeviceSynchronize());
         HJ_HIP(hipMemcpy(&v, c->meta + 1, 8, hipMemcpyDeviceToHost));
         c->dup_checked = true;
@@ -1324,7 +1359,7 @@ int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->dual = false;
     c->probe_used = -1;
     c->join_ran = false;
-    c->memo.valid = false;
+    c->memo.invalidate();
     c->plan = pl;
     c->routed = true;
     c->dup_checked = false;
@@ -1332,7 +1367,7 @@ int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     record(c, kEvInit0, st);
     HJ_HIP(hipMemsetAsync(c->meta, 0, 4 * sizeof(unsigned long long), st));
     record(c, kEvInit1, st);
-    HJ_HIP(hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, 1 << sub_bits, pl,
+    HJ_RADIX(c, st, hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, 1 << sub_bits, pl,
                                       radix_work(c), bucket_set(c->rset), st));
     HJ_HIP(hj::radix_sample(true, pl, bucket_set(c->rset), c->meta + 2, st));
     record(c, kEvBuild1, st);
@@ -1357,14 +1392,14 @@ int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->probe_used = HJ_STRATEGY_RADIX;   // (radix_join zeroes d_count)
     HJ_TRY(ensure_radix_scratch(c, c->sset, n, 16, c->plan));
     record(c, kEvProbe0, st);
-    HJ_HIP(hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, nbins, c->plan,
+    HJ_RADIX(c, st, hj::radix_partition_routed(tuples, n, (const unsigned long long *)d_counts, nsrc, nbins, c->plan,
                                       radix_work(c), bucket_set(c->sset), st));
     record(c, kEvProbeMid, st);
     // bins [bin0, bin0 + nbins): partitions [bin0, bin0 + nbins) << bits[1] of R
     hj::BucketSet r = bucket_set(c->rset);
     r.rstart += (size_t)bin0 << c->plan.bits[1];
     const bool stream_shape = n >= 8 * c->n_build;
-    HJ_HIP(hj::radix_join(true, c->plan, radix_work(c), r, bucket_set(c->sset), c->sset.max_runs,
+    HJ_RADIX(c, st, hj::radix_join(true, c->plan, radix_work(c), r, bucket_set(c->sset), c->sset.max_runs,
                           (unsigned *)c->work_start.p, c->work_desc.p, out_r, out_s, out_cap,
                           (unsigned long long *)d_count, c->meta + 1, false, st, c->meta + 2, stream_shape,
                           nbins << c->plan.bits[1]));
@@ -1679,6 +1714,18 @@ int hj_dev_select_f32(hj_ctx *c, const float *in, int64_t n, int cmp, float valu
 int hj_dev_select_i64(hj_ctx *c, const int64_t *in, int64_t n, int cmp, int64_t value, int64_t *out,
                       int64_t *out_row, int64_t out_cap, uint64_t *d_count, void *stream) {
     return do_select<int64_t>(c, in, n, cmp, value, out, out_row, out_cap, d_count, (hipStream_t)stream);
+}
+
+int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void *stream) {
+    if (shape != HJ_COPY_PERSISTENT && shape != HJ_COPY_FLAT) HJ_FAIL(HJ_ERR_ARG, "bad copy shape");
+    if (rows < 0) HJ_FAIL(HJ_ERR_ARG, "negative row count");
+    if (rows > 0 && (!in || !out || (((uintptr_t)in | (uintptr_t)out) & 15)))
+        HJ_FAIL(HJ_ERR_ARG, "copy buffers must be non-null and 16-B aligned");
+    int dev = 0, cus = 0;
+    HJ_HIP(hipGetDevice(&dev));
+    HJ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HJ_HIP(hj::launch_stream_copy(in, out, rows, shape, cus, (hipStream_t)stream));
+    return HJ_OK;
 }
 
 int64_t hj_select_f32(float *, float *in, int64_t in_off, int64_t in_size, int64_t in_stride, float value, float *,

@@ -251,6 +251,8 @@ hipError_t launch_select_f32(const float *in, long long n, int op, float c, floa
 hipError_t launch_select_i64(const long long *in, long long n, int op, long long c, long long *out,
                              long long *out_row, long long cap, unsigned long long *count, unsigned long long *tiles,
                              unsigned long long *sums, hipStream_t st);
+// copy floors (hj_dev_stream_copy): shape 0 persistent (cus workgroups), 1 flat
+hipError_t launch_stream_copy(const void *in, void *out, long long rows, int shape, int cus, hipStream_t st);
 
 // nested-loop.mlir result rows (hj_kernels.hip)
 hipError_t launch_key_col_i32(const int *t, long long rows, long long ld, int *out, hipStream_t st);

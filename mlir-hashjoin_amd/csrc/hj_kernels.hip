@@ -1067,4 +1067,59 @@ hipError_t launch_select_i64(const long long *in, long long n, int op, long long
     return launch_select_t<long long>(in, n, op, c, out, out_row, cap, count, tiles, sums, st);
 }
 
+// ------------------------------------------------------------ copy floors
+// The box's own streamed-copy rate, so a bench line can say how far each
+// phase is from it.  16-B rows, non-temporal
+// loads and stores (the partition passes' access flavour).
+typedef unsigned long long cp_u64;
+typedef __attribute__((ext_vector_type(2))) unsigned long long cp_v2;
+
+__device__ __forceinline__ cp_v2 cp_ld(const cp_v2 *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void cp_st(cp_v2 *p, cp_v2 v) { __builtin_nontemporal_store(v, p); }
+
+// one row per thread over the whole grid (n / 256 workgroups): the chip's
+// best copy shape (6.2-6.4 TB/s, profiles/r04_copy_and_interleave.txt)
+__global__ __launch_bounds__(256) void k_copy_flat(const cp_v2 *__restrict__ in, cp_v2 *__restrict__ out, cp_u64 n) {
+    const cp_u64 i = (cp_u64)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) cp_st(out + i, cp_ld(in + i));
+}
+
+// the partition passes' loop shape: one 1024-thread workgroup per CU walks a
+// contiguous range of 4096-row tiles with the next tile's loads in flight
+// during this tile's stores
+constexpr int kCpNT = 1024, kCpIT = 4;
+__global__ __launch_bounds__(kCpNT) void k_copy_persistent(const cp_v2 *__restrict__ in, cp_v2 *__restrict__ out,
+                                                           cp_u64 n) {
+    constexpr cp_u64 T = (cp_u64)kCpNT * kCpIT;
+    const cp_u64 tiles = n / T;
+    const cp_u64 t0 = (cp_u64)blockIdx.x * tiles / gridDim.x, t1 = (cp_u64)(blockIdx.x + 1) * tiles / gridDim.x;
+    cp_v2 r[kCpIT], q[kCpIT];
+    if (t0 < t1)
+#pragma unroll
+        for (int i = 0; i < kCpIT; ++i) r[i] = cp_ld(in + t0 * T + (cp_u64)i * kCpNT + threadIdx.x);
+    for (cp_u64 t = t0; t < t1; ++t) {
+        if (t + 1 < t1)
+#pragma unroll
+            for (int i = 0; i < kCpIT; ++i) q[i] = cp_ld(in + (t + 1) * T + (cp_u64)i * kCpNT + threadIdx.x);
+#pragma unroll
+        for (int i = 0; i < kCpIT; ++i) cp_st(out + t * T + (cp_u64)i * kCpNT + threadIdx.x, r[i]);
+#pragma unroll
+        for (int i = 0; i < kCpIT; ++i) r[i] = q[i];
+    }
+    // rows past the last whole tile (n % T): the last workgroup, one per thread
+    if (blockIdx.x == gridDim.x - 1)
+        for (cp_u64 i = tiles * T + threadIdx.x; i < n; i += kCpNT) cp_st(out + i, cp_ld(in + i));
+}
+
+hipError_t launch_stream_copy(const void *in, void *out, long long rows, int shape, int cus, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    const cp_v2 *s = (const cp_v2 *)in;
+    cp_v2 *d = (cp_v2 *)out;
+    if (shape == 0)
+        hipLaunchKernelGGL(k_copy_persistent, dim3(cus > 0 ? cus : 1), dim3(kCpNT), 0, st, s, d, (cp_u64)rows);
+    else
+        hipLaunchKernelGGL(k_copy_flat, dim3(grid_for(rows, 256)), dim3(256), 0, st, s, d, (cp_u64)rows);
+    return hipGetLastError();
+}
+
 }  // namespace hj

@@ -333,8 +333,18 @@ __global__ __launch_bounds__(kLbThreads) void k_scan_lb(u64 *a, u64 n, u64 *stat
         run += v[i];
     }
     __syncthreads();
-    if (threadIdx.x == 0 && atomicAdd(&state[nt + 1], 1ull) == (u64)nt - 1ull)
-        for (unsigned k = 0; k < nt + 2; ++k) atomicExch(&state[k], 0ull);
+    // The done count is what lets the last workgroup clear every word, so it
+    // must not overtake this tile's own publishes (the atomicExch calls on
+    // state[t] above): a release fence orders them, and the clearing thread's acquire fence
+    // orders every tile's publish before its clears.  Two
+    // fences per workgroup, once per scan.
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&state[nt + 1], 1ull) == (u64)nt - 1ull) {
+            __threadfence();
+            for (unsigned k = 0; k < nt + 2; ++k) atomicExch(&state[k], 0ull);
+        }
+    }
 }
 
 // --------------------------------------------------------------- partition pass
@@ -3508,6 +3518,31 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     return hipGetLastError();
 }
 
+// radix_detect's deferred partitions: rows[1] += the rows of every listed
+// item (sum of its R run counts); the last workgroup to finish sets
+// *dup_flag when the self-join's pair count rows[0] exceeds them.
+__global__ __launch_bounds__(256) void k_defer_rows(const unsigned *list, const unsigned *list_n, const ItemDesc *desc,
+                                                    const u64 *runs, u64 *rows, u64 *dup_flag) {
+    __shared__ u64 wsum[16];
+    const unsigned n = *list_n;
+    u64 s = 0;
+    for (unsigned x = blockIdx.x; x < n; x += gridDim.x) {
+        const ItemDesc d = desc[list[x]];
+        for (u64 i = d.r_lo + threadIdx.x; i < d.r_hi; i += 256) s += runs[i] & 127u;
+    }
+    u64 tot;
+    (void)block_excl_scan<256>(s, wsum, &tot);
+    if (threadIdx.x == 0) {
+        if (tot) atomicAdd(&rows[1], tot);
+        __threadfence();
+        if (atomicAdd(&rows[2], 1ull) == (u64)gridDim.x - 1ull) {
+            __threadfence();
+            const u64 pairs = atomicAdd(&rows[0], 0ull), have = atomicAdd(&rows[1], 0ull);
+            if (pairs > have) atomicExch(dup_flag, 1ull);
+        }
+    }
+}
+
 hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, const BucketSet &r, unsigned *work_start,
                         void *desc, unsigned long long *dup_flag, const unsigned long long *sample, hipStream_t st) {
     // one item per non-empty partition of the WHOLE build side (a work map
@@ -3560,6 +3595,24 @@ hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, con
     else
         hipLaunchKernelGGL((k_join<false, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
                            dim3(512), 0, st, a);
+    // That build flags a key repeated inside one of its rounds only.  The
+    // exact answer for a deferred (oversized) partition: the count-only
+    // self-join of its rows across every round (S = the partition itself)
+    // has more pairs than the partition has rows iff some key repeats
+    // (ADVICE r04).  pcur[0] = pairs, pcur[1] = rows of the deferred items,
+    // pcur[2] = k_defer_rows's done count.
+    hipError_t e = hipMemsetAsync(ws.pcur, 0, 3 * sizeof(u64), st);
+    if (e != hipSuccess) return e;
+    a.empty_s = false;
+    a.counter = ws.pcur;
+    if (wide)
+        hipLaunchKernelGGL((k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
+                           dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_join<false, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
+                           dim3(512), 0, st, a);
+    hipLaunchKernelGGL(k_defer_rows, dim3(2 * cu_count()), dim3(256), 0, st, (const unsigned *)(defer_n + 1),
+                       (const unsigned *)defer_n, (const ItemDesc *)desc, (const u64 *)r.runs, ws.pcur, dup_flag);
     return hipGetLastError();
 }
 

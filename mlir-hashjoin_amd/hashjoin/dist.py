@@ -324,8 +324,9 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     partition / build_tuples / probe_tuples methods).  Returns this rank's
     share of the result (out_r, out_s) = (R.pay, S.pay): the pairs of keys it
     owns (shuffle) or of its own S rows (replicate).  `phases`, if a dict,
-    receives events (start, routed, built, probed) for timing (CUDA events on
-    GPU tensors, else host timestamps), "rows" = (R rows built, S rows
+    receives events (start, s_route, routed, built, probed) for timing (CUDA
+    events on GPU tensors, else host timestamps; s_route -> routed is S's
+    routing, absent when R is replicated), "rows" = (R rows built, S rows
     probed) and "mode" = "shuffle" | "replicate".  n_build_global: |R| over
     all ranks when the caller knows it (the same value on every rank); it
     saves the all-reduce and host round trip that otherwise decide between
@@ -370,6 +371,7 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
         nb = 1 << sub
         send_r, cr = hj.route(rkey, rpay, world, sub)
         xr = RoutedExchange(send_r, cr, nb, group, max_rows, self_p2p)
+        ev("s_route")   # S's share of the route phase: its first partition pass happens here
         send_s, cs = hj.route(skey, spay, world, sub)
         xs = RoutedExchange(send_s, cs, nb, group, max_rows, self_p2p, parts=s_parts)
         ev("routed")
@@ -390,6 +392,7 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
     _dbg("route", rkey.numel(), skey.numel())
     send_r, cr = hj.partition(rkey, rpay, world)
     xr = Exchange(send_r, cr, group, max_rows, self_p2p)
+    ev("s_route")
     send_s, cs = hj.partition(skey, spay, world)
     xs = Exchange(send_s, cs, group, max_rows, self_p2p, parts=s_parts)
     ev("routed")

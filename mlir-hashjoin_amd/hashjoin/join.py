@@ -393,6 +393,20 @@ def device_info(device=0):
     return dict(zip(keys, [int(x) for x in a]))
 
 
+COPY_SHAPES = {"persistent": 0, "flat": 1}
+
+
+def stream_copy(src, dst, shape="persistent", stream=None):
+    """Copy 16-B rows src -> dst on the device in one of the two reference
+    copy shapes of hj_dev_stream_copy (the bench's copy floor)."""
+    _need_cuda(src, dst)
+    if src.numel() * src.element_size() != dst.numel() * dst.element_size() or src.numel() * src.element_size() % 16:
+        raise ValueError("stream_copy needs equal-sized buffers of whole 16-B rows")
+    rows = src.numel() * src.element_size() // 16
+    check(lib.hj_dev_stream_copy(_ptr(src), _ptr(dst), rows, COPY_SHAPES[shape], _stream(src.device, stream)),
+          "hj_dev_stream_copy")
+
+
 def partition_of(key: int, nparts: int) -> int:
     """Owner of a key under the routing hash (host function of libhj.so)."""
     return int(lib.hj_partition_of(int(key), int(nparts)))

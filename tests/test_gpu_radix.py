@@ -606,3 +606,30 @@ def test_radix_duplicates_in_unprobed_partitions(hj, oracle, wide, dups):
         assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
     assert len(o[0]) == 8
     assert hj.has_duplicates() == dups
+
+
+@pytest.mark.parametrize("wide", [True, False])
+@pytest.mark.parametrize("dups", [False, True])
+def test_radix_duplicates_across_build_rounds(hj, oracle, wide, dups):
+    """has_duplicates() when the only repeated build key sits in a partition
+    too large for one LDS table (2 radix bits: ~10k rows per partition,
+    deferred to k_join's list mode, built in rounds of 2560 rows) with its two
+    copies in different rounds: the detect path's self-join count
+    finds it; unique keys stay unique."""
+    n = 40000
+    rng = np.random.default_rng(777 + (1 if wide else 0))
+    rk = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
+    if dups:
+        rk[n - 1] = rk[0]   # first and last build row: read in different rounds
+    sk = rk[1:9].copy()     # 8 probe rows, none with the repeated key
+    rp = np.arange(n, dtype=np.int64) * 3 + 1
+    sp = np.arange(len(sk), dtype=np.int64) + 5
+    if wide:
+        o = run(hj, rk, rp, sk, sp, 2)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=1000))
+    else:
+        o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 2)
+        ex = oracle.chained_join_i32(rk.astype(np.int32), sk.astype(np.int32), H=1000)
+        assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
+    assert len(o[0]) == 8
+    assert hj.has_duplicates() == dups
