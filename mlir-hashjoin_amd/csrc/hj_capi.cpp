@@ -195,6 +195,7 @@ struct hj_ctx {
     bool join_ran = false, join_wide = false, join_stream = false;
     bool routed = false;   // the current build came from hj_dev_build_routed_i64 (plan.skip owner bits)
     bool dup_checked = false;   // hj_ctx_build_has_duplicates ran its DETECT build for this build
+    bool host_building = false;  // host_join's build is running (do_build keeps the memo's input copies)
 };
 
 namespace {
@@ -359,7 +360,10 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     c->join_ran = false;
     c->dup_checked = false;
     c->routed = false;
-    c->memo.invalidate();   // (hj_count_*'s kept table is gone)
+    // (hj_count_*'s kept table is gone; a host join's own build keeps the
+    // EXACT copies it has just taken of its inputs)
+    if (c->host_building) c->memo.valid = false;
+    else c->memo.invalidate();
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
@@ -888,7 +892,10 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
         HJ_TRY(upload_rel(c, layout, r, dr_buf, &rsrc));
         HJ_TRY(upload_rel(c, layout, s, ds_buf, &ssrc));
     }
-    HJ_TRY(do_build(c, layout, rsrc, st));
+    c->host_building = true;
+    const int brc = do_build(c, layout, rsrc, st);
+    c->host_building = false;
+    HJ_TRY(brc);
     if (mode != kHostCount) {
         HJ_TRY(host_probe_all(c, layout, ssrc, (size_t)esz, s.n, m));
         *d_or = c->dbuf[2];

@@ -552,6 +552,24 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
             // two consecutive rows per lane: one 16-B load from each column
             // (rows lo + 2 * (i * NT + t) + {0, 1}; order inside a tile is free)
             const u64 *kc = (const u64 *)a.in.key, *pc = (const u64 *)a.in.pay;
+            if (a.cols_aligned && tlo + (u64)kTile <= a.n) {
+                // a whole, aligned tile (a uniform branch): no per-lane guard,
+                // so the loads are not EXEC-masked beside the guarded ones
+                // below -- two masked paths writing the same registers made
+                // the compiler wait vmcnt(0) (the previous tile's stores)
+                // before issuing them
+#pragma unroll
+                for (int i = 0; i < IT / 2; ++i) {
+                    const u64 r = tlo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
+                    const ulonglong2 k2 = ld_s<kNtPassLd>((const ulonglong2 *)(kc + r));
+                    const ulonglong2 p2 = ld_s<kNtPassLd>((const ulonglong2 *)(pc + r));
+                    row[2 * i] = R::make(k2.x, p2.x);
+                    row[2 * i + 1] = R::make(k2.y, p2.y);
+                    br[2 * i] = 0u;
+                    br[2 * i + 1] = 0u;
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < IT / 2; ++i) {
                 const u64 r = tlo + 2ull * ((u64)i * kPassThreads + threadIdx.x);
@@ -636,6 +654,12 @@ __global__ __launch_bounds__(NT) void k_pass(PassArgs a) {
             load_tile(tlo, row, br);
         }
     }
+    // The first tile's rows arrive here, before the loop: otherwise the
+    // compiler's wait counting merges "rows still loading" from this entry
+    // into every iteration and waits vmcnt(0) -- i.e. for the NEXT tile's
+    // loads, issued after the count -- before the scatter writes the rows to
+    // the stage, which left those loads in flight during the scan only.
+    __builtin_amdgcn_s_waitcnt(0);
     u64 ph[6] = {0, 0, 0, 0, 0, 0}, tp = 0;
     auto mark = [&](int k) {
         if constexpr ((ABL & 8) != 0) {
