@@ -53,6 +53,10 @@ CONFIGS = {
               "reference workload 1: 10M x 10M i32 keys uniform in [1, 100k] (~1e9 result rows)"),
     "REF-B": (100_000_000, 100_000_000, "ref1e9", "int32",
               "reference workload 2: 100M x 100M i32 keys uniform in [1, 1e9] (~1e7 result rows)"),
+    # workload 1's key distribution as int64 key + payload columns: most build
+    # keys repeat (~100 copies), the int64 rows' mostly-repeated join path
+    "REF-A64": (10_000_000, 10_000_000, "ref100k64", "int64",
+                "workload 1's keys as int64 key+payload: 10M x 10M keys uniform in [1, 100k] (~1e9 result rows)"),
 }
 # the reference's own times for those workloads (join-performances.md; sm_86, all four kernels + module loads)
 REFERENCE_PUBLISHED = {
@@ -353,6 +357,10 @@ def gen_inputs(hashjoin, a, NR, NS, distn, r0, nr, s0, ns):
     if distn == "zipf":
         rk, rp, _, _ = hashjoin.gen_pkfk(a.seed, NR, NS, 1.0, r0, nr, s0, 0)
         sk, sp = hashjoin.gen_zipf(a.seed, NR, NS, 0.9, s0, ns)
+        return rk, rp, sk, sp
+    if distn == "ref100k64":
+        rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 100_000, nr, i0=r0)
+        sk, sp = hashjoin.gen_uniform_i64(a.seed, 2, 1, 100_000, ns, i0=s0)
         return rk, rp, sk, sp
     if distn == "uniform30":
         rk, rp = hashjoin.gen_uniform_i64(a.seed, 1, 1, 1 << 30, nr, i0=r0)

@@ -1222,6 +1222,11 @@ struct JoinArgs {
     unsigned *next_item = nullptr;
     // k_join (radix_detect): build only -- every item's S chunk is empty
     bool empty_s = false;
+    // a LIST launch that takes EVERY item instead when the build-time sample
+    // says most build keys repeat (mode 2): the kernel the fast launch
+    // before it left to it (k_join for int64 rows, k_join_grp for i32 rows),
+    // so that launch and the mode-2 one are one launch (no exit-only launch)
+    bool all_if_mode2 = false;
 };
 
 constexpr unsigned kModeUnique = 1u, kModeSome = 2u, kModeMostlyRepeated = 4u;
@@ -1244,6 +1249,11 @@ __host__ __device__ __forceinline__ int sample_mode(u64 rows, u64 repeats) {
 __device__ __forceinline__ bool join_runs(const JoinArgs &a) {
     const int m = a.sample ? sample_mode(sload(a.sample), sload(a.sample + 1)) : 0;
     return (a.modes >> m) & 1u;
+}
+// a LIST kernel's item source: the list, or every item (all_if_mode2 and a
+// mode-2 sample)
+__device__ __forceinline__ bool join_uses_list(const JoinArgs &a) {
+    return !(a.all_if_mode2 && a.sample && sample_mode(sload(a.sample), sload(a.sample + 1)) == 2);
 }
 
 // Build-side sample, launched after R's partition (radix_sample): workgroup
@@ -1368,7 +1378,8 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     constexpr int NW = NT / 64;
     __shared__ unsigned s_cw[SI * NW];        // per (row slot, wave) match counts, then offsets
 
-    const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
+    const bool use_list = LIST && join_uses_list(a);
+    const unsigned total = use_list ? *a.list_n : a.work_start[a.P];
     unsigned w = blockIdx.x;
     if (w >= total) return;
     const T *rrows = (const T *)a.r;
@@ -1376,7 +1387,7 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     PT *orr = (PT *)a.out_r;
     PT *oss = (PT *)a.out_s;
     auto item = [&](unsigned x) {
-        ItemDesc d = LIST ? a.desc[a.list[x]] : a.desc[x];
+        ItemDesc d = use_list ? a.desc[a.list[x]] : a.desc[x];
         if (a.empty_s) d.s_hi = d.s_lo;
         return d;
     };
@@ -2736,7 +2747,8 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     __shared__ u64 wsum[16];
     __shared__ u64 s_base;
     __shared__ unsigned s_rep;
-    const unsigned total = LIST ? *a.list_n : a.work_start[a.P];
+    const bool use_list = LIST && join_uses_list(a);
+    const unsigned total = use_list ? *a.list_n : a.work_start[a.P];
     if (!join_runs(a)) return;
     const u64 *rrows = (const u64 *)a.r;
     const u64 *srows = (const u64 *)a.s;
@@ -2776,7 +2788,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
         }
     };
     for (unsigned w = blockIdx.x; w < total; w += gridDim.x) {
-        const unsigned wi = LIST ? a.list[w] : w;
+        const unsigned wi = use_list ? a.list[w] : w;
         const ItemDesc it = sload(a.desc + wi);
         if (it.r_hi - it.r_lo > (u64)rmax) {   // uniform
             if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = wi;
@@ -3488,16 +3500,14 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             HJ_WR((k_join_u<true, true, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>),
                   (k_join_u<true, false, kTableLog, kStreamNT, kStreamRI, kStreamSI, kStreamWPS>), kStreamNT);
         } else {
-            // k_join_b unless most build keys repeat (its multi-match walks
-            // lose to k_join_u's per-row walks there).  (Both bodies in one
-            // kernel, the sample choosing, spilled 20 B at the 80-VGPR cap of
-            // 6 waves per SIMD: the unchosen kernel's exit launch stays.)
+            // k_join_b unless most build keys repeat; then k_join takes every
+            // item (below, the same launch that takes k_join_b's deferrals:
+            // no exit-only launch of a kernel the sample did not choose).
+            // (k_join_u served mode 2 before round 5 in a launch of its own;
+            // both bodies in one kernel spilled 20 B at the 80-VGPR cap.)
             a.modes = kModeUnique | kModeSome;
             HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
-            a.modes = kModeMostlyRepeated;
-            HJ_WR((k_join_u<true, true, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>),
-                  (k_join_u<true, false, kTableLog, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
         }
     } else {
         // i32 rows: k_join_b (keys and row ids apart in LDS: a bucket's 4
@@ -3518,21 +3528,25 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
                                    dim3(gn), dim3(kNarrowNT), 0, st, a);
             a.next_item = nullptr;
         }
+        // k_join_grp: k_join_b's deferrals, or every item when most build
+        // keys repeat (one launch either way)
+        a.modes = kModesAll;
         a.list = defer_n + 1;
         a.list_n = defer_n;
+        a.all_if_mode2 = true;
         a.defer = defer2_n + 1;
         a.defer_n = defer2_n;
         HJ_WR((k_join_grp<true, kGrpNT, kGrpRI, kGrpSI, true>), (k_join_grp<false, kGrpNT, kGrpRI, kGrpSI, true>), kGrpNT);
-        a.modes = kModeMostlyRepeated;
-        HJ_WR((k_join_grp<true, kGrpNT, kGrpRI, kGrpSI, false>), (k_join_grp<false, kGrpNT, kGrpRI, kGrpSI, false>),
-              kGrpNT);
+        a.all_if_mode2 = false;
     }
     // what the kernels above deferred (INT64_MIN build keys, oversized
     // partitions, full tables): k_join over that list, a persistent grid that
-    // exits at once when it is empty
+    // exits at once when it is empty -- and, for int64 rows outside the
+    // stream shape, every item when the sample says most build keys repeat
     a.modes = kModesAll;
     a.list = wide ? defer_n + 1 : defer2_n + 1;
     a.list_n = wide ? defer_n : defer2_n;
+    a.all_if_mode2 = wide && !stream_shape;
     if (wide) HJ_WR((k_join<true, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
                     (k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), 512);
     else HJ_WR((k_join<false, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
@@ -3655,7 +3669,7 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
     const int m = sample_mode(rows, repeats);
     if (wide) {
         if (stream) return HJ_JOIN_KERNEL_STREAM;
-        return m == 2 ? HJ_JOIN_KERNEL_LINEAR : HJ_JOIN_KERNEL_BUCKETED;
+        return m == 2 ? HJ_JOIN_KERNEL_GENERAL : HJ_JOIN_KERNEL_BUCKETED;
     }
     return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_BUCKETED;
 }

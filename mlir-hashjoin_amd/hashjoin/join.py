@@ -105,12 +105,12 @@ class HashJoin:
             check(r, "hj_ctx_build_has_duplicates")
         return bool(r)
 
-    JOIN_KERNELS = {1: "k_join_b", 2: "k_join_u", 3: "k_join_u_stream", 4: "k_join_grp"}
+    JOIN_KERNELS = {1: "k_join_b", 2: "k_join_u", 3: "k_join_u_stream", 4: "k_join_grp", 5: "k_join"}
 
     @property
     def join_kernel(self):
         """Kernel of the last radix join (hj_ctx_join_kernel): 'k_join_b',
-        'k_join_u', 'k_join_u_stream', 'k_join_grp', or None (no radix join)."""
+        'k_join_u_stream', 'k_join_grp', 'k_join', or None (no radix join)."""
         r = lib.hj_ctx_join_kernel(self._ctx)
         if r < 0:
             check(r, "hj_ctx_join_kernel")
