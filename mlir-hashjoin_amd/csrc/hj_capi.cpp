@@ -136,7 +136,7 @@ struct hj_ctx {
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
     SetBufs rset, sset, tset;   // R and S final partitions, ping set of multi-pass plans
-    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, wstart, work_start, work_desc, scan_sums, scan_state;
+    Buf nb, pcur, rcur, tile_start, tile_owner, tdesc, wstart, work_start, work_desc, scan_sums, scan_state, raw_cnt;
     Buf slow;   // global-table probe: tiles for the general path
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
@@ -316,6 +316,7 @@ int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const h
     HJ_TRY(ensure_buf(c->work_start, (size_t)hj::radix_work_words(pl, fin.max_runs) * 4));
     HJ_TRY(ensure_buf(c->work_desc, items * hj::radix_item_desc_bytes()));
     HJ_TRY(ensure_buf(c->scan_sums, ((P + 1) / 8192 + 2) * 8));
+    HJ_TRY(ensure_buf(c->raw_cnt, 2 * hj::kRawCntWords * 8));
     {
         // the one-launch scan's tile words: zero on allocation, and every
         // scan leaves them zero
@@ -338,6 +339,7 @@ hj::RadixWork radix_work(hj_ctx *c) {
     w.wstart = (unsigned *)c->wstart.p;
     w.scan_sums = (unsigned long long *)c->scan_sums.p;
     w.scan_state = (unsigned long long *)c->scan_state.p;
+    w.raw_cnt = (unsigned long long *)c->raw_cnt.p;
     return w;
 }
 
@@ -1105,7 +1107,7 @@ void hj_ctx_destroy(hj_ctx *c) {
     if (c->host_stream) (void)hipStreamDestroy(c->host_stream);
     for (SetBufs *sb : {&c->rset, &c->sset, &c->tset})
         for (Buf *b : {&sb->rows, &sb->bbin, &sb->bfill, &sb->runs, &sb->rstart}) free_buf(*b);
-    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums, &c->scan_state,
+    for (Buf *b : {&c->nb, &c->pcur, &c->rcur, &c->tile_start, &c->tile_owner, &c->tdesc, &c->wstart, &c->work_start, &c->work_desc, &c->scan_sums, &c->scan_state, &c->raw_cnt,
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
                    &c->route_hist, &c->route_sums})
         free_buf(*b);

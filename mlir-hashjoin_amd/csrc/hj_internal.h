@@ -165,7 +165,11 @@ struct RadixWork {                 // scratch shared by the partition passes
     unsigned *wstart;              // >= 1025: per-workgroup bucket id ranges of a pass
     unsigned long long *scan_sums; // >= P / 8192 + 2
     unsigned long long *scan_state;// >= P / 1024 + 4, zero between calls (the one-launch scan's tile words)
+    // 2 x (kRawCntWords): a small pass's raw run counts by pass parity, when
+    // the next pass's plan launch scans them itself (null: a scan launch)
+    unsigned long long *raw_cnt = nullptr;
 };
+constexpr unsigned long long kRawCntWords = 4097;   // kPlanSegs + 1 (hj_radix.hip)
 
 struct RadixNeed {                 // sizes of one bucket set
     unsigned long long buckets, rows;

@@ -1083,7 +1083,11 @@ struct PlaceArgs {
     const u64 *rstart;
     u64 *rcur, *runs;
     int P;
+    // raw run counts (P + 1 <= kRawCntWords) still to be scanned: k_place_plan
+    // scans them itself into rstart (null: rstart is already scanned)
+    const u64 *raw = nullptr;
 };
+static_assert(kRawCntWords == (u64)kPlanSegs + 1, "raw count words: a plan's segments + 1");
 
 __device__ __forceinline__ void bplace_body(const PlaceArgs &pa, unsigned bid) {
     const unsigned *bbin = pa.bbin, *bfill = pa.bfill, *nb = pa.nb;
@@ -1189,7 +1193,38 @@ __global__ __launch_bounds__(1024) void k_bplace(PlaceArgs pa) { bplace_body(pa,
 // starts of pass p: pass p's run placement (blocks [0, nplace)) and pass p +
 // 1's plan (the rest).  (They use separate bucket-count words and cursor
 // arrays: the plan zeroes pass p + 1's while pass p's are in use.)
+// pa.raw: every block scans the previous pass's raw run counts (<= kPlanSegs
+// + 1 of them) into LDS and both bodies read the starts from there; block 0
+// also writes them to pa.rstart for the kernels after this one.  (This is
+// the scan launch the listing of a small pass had of its own.)
 __global__ __launch_bounds__(1024) void k_place_plan(PlaceArgs pa, unsigned nplace, TilePlanArgs tp) {
+    __shared__ u64 rs[kPlanSegs + 1];
+    if (pa.raw) {
+        __shared__ u64 wsum[16];
+        constexpr int PER = (kPlanSegs + 1 + 1023) / 1024;
+        const int n = pa.P + 1;
+        u64 v[PER], sum = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x * PER + i;
+            v[i] = e < n ? pa.raw[e] : 0ull;
+            sum += v[i];
+        }
+        u64 total;
+        u64 run = block_excl_scan<1024>(sum, wsum, &total);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = threadIdx.x * PER + i;
+            if (e < n) {
+                rs[e] = run;
+                if (blockIdx.x == 0) ((u64 *)pa.rstart)[e] = run;
+            }
+            run += v[i];
+        }
+        __syncthreads();
+        pa.rstart = rs;
+        tp.rstart = rs;
+    }
     if (blockIdx.x < nplace) bplace_body(pa, blockIdx.x);
     else tile_plan_body(tp, blockIdx.x - nplace, gridDim.x - nplace);
 }
@@ -3286,9 +3321,13 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         a.tile_rows = pass_tile_rows(fb, wide);
         a.wstart = ws.wstart;
         // the pass counts its buckets' runs per partition into dst.rstart;
-        // the plan kernel zeroes them and the placement cursors first
+        // the plan kernel zeroes them and the placement cursors first.  A
+        // small pass followed by another counts into ws.raw_cnt instead, and
+        // the next pass's plan launch (k_place_plan) scans them itself.
         const u64 P = (u64)nseg << fb;
-        a.rcnt = n > 0 ? dst.rstart : nullptr;
+        const bool fuse = ws.raw_cnt && pass + 1 < pl.passes && P <= (u64)kPlanSegs;
+        u64 *cnt = fuse ? ws.raw_cnt + (u64)(pass & 1) * kRawCntWords : dst.rstart;
+        a.rcnt = n > 0 ? cnt : nullptr;
         if (grid > 1023) return hipErrorInvalidValue;   // plans: one thread per workgroup + 1
         const unsigned zgrid = blocks_for(P + 1, 1024);
         if (prev && nseg <= kPlanSegs) {
@@ -3300,7 +3339,7 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
             if (pg < zgrid) pg = zgrid;
             if (pg > 1024) pg = 1024;
             TilePlanArgs tp{a, (const u64 *)prev->rstart, grid, (unsigned)tb, ws.tile_start, (TileDesc *)ws.tdesc,
-                            ws.wstart, dst.rstart, rcur, P + 1};
+                            ws.wstart, cnt, rcur, P + 1};
             if (pending) hipLaunchKernelGGL(k_place_plan, dim3(np_prev + pg), dim3(1024), 0, st, pa_prev, np_prev, tp);
             else hipLaunchKernelGGL(k_tile_plan, dim3(pg), dim3(1024), 0, st, tp);
             pending = false;
@@ -3319,7 +3358,7 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
                 a.tdesc = (const TileDesc *)ws.tdesc;
             }
             hipLaunchKernelGGL(k_id_plan, dim3(zgrid < 1024 ? zgrid : 1024), dim3(1024), 0, st, a, prev != nullptr, grid,
-                               ws.wstart, dst.rstart, rcur, P + 1);
+                               ws.wstart, cnt, rcur, P + 1);
         }
         if (n > 0) {
 #define HJ_PASS(W, FORM)                                                                                    \
@@ -3344,9 +3383,10 @@ hipError_t radix_passes(const SrcDev &src, u64 n, bool wide, const RadixPlan &pl
         }
         // runs fit by construction (max_runs >= max_rows / 64 + max_buckets)
         if (dst.max_runs < (dst.max_rows >> kRunLog) + dst.max_buckets) return hipErrorInvalidValue;
-        scan_one(dst.rstart, P + 1, ws, st);
+        if (!fuse) scan_one(dst.rstart, P + 1, ws, st);
         pa_prev = PlaceArgs{(const unsigned *)dst.bbin, (const unsigned *)dst.bfill, (const unsigned *)nbw, a.max_buckets,
-                            pl.pbl[pass], (const u64 *)dst.rstart, rcur, dst.runs, (int)P};
+                            pl.pbl[pass], (const u64 *)dst.rstart, rcur, dst.runs, (int)P,
+                            fuse ? (const u64 *)cnt : nullptr};
         np_prev = blocks_for(dst.max_buckets, 1024 * kListPer);
         pending = true;
         const hipError_t e = hipGetLastError();
