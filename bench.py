@@ -625,6 +625,9 @@ def main():
             "algorithmic_bytes": nr * 32 * max(1, hj.radix_passes if strategy == "radix" else 1),
             "ms": round(build_ms, 4),
         },
+        # the bucket sets' row buffers, probed and redrawn at allocation
+        # (hj_placement_stats; done in the untimed first call)
+        "placement": hashjoin.placement_stats(),
         "device": {"name": torch.cuda.get_device_name(local), **info,
                    "peak_used_gbs": HBM_PEAK_GBS,
                    "peak_note": "8.0 TB/s spec (MI355X_MICROARCH.md); peak_mb_per_s = hipDeviceProp "

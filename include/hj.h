@@ -261,6 +261,16 @@ int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_
 #define HJ_COPY_FLAT 1
 int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void *stream);
 
+/* Placement of the radix bucket sets' row buffers (diagnostics, no reference
+ * counterpart).  A row buffer of >= 4 GiB is probed when allocated: the
+ * partition pass's write pattern against a flat write of the same bytes
+ * (some physical placements run the pattern 25-35 % slower), redrawn up to 12
+ * times while slow, best draw kept; HJ_PLACEMENT_PROBE=0 in the environment
+ * turns the probe off.  Process-wide counts since load: draws probed, draws
+ * rejected, and the pattern/flat ratio of the last and of the worst kept
+ * buffer (0 when none was probed).  Any pointer may be null. */
+void hj_placement_stats(long long *probes, long long *rejected, double *last_kept, double *worst_kept);
+
 /* Out-of-core join of HOST-resident int64 key/payload columns (relations
  * larger than HBM; the reference leaves the partitioned join out,
  * projectDescription.md:23-24).  When R does not fit device_budget bytes

@@ -267,9 +267,95 @@ void free_buf(Buf &b) {
     b.bytes = 0;
 }
 
+// Placement of the bucket sets' row buffers (the partition passes' only
+// destinations).  The passes write each tile's rows as one line into each of
+// ~512 open buckets per workgroup, and into some physical placements of a
+// buffer that pattern runs 25-35 % slower than a flat write (a property of
+// the allocation, bimodal: 4-10 of 12 fresh 6 GiB buffers on one box,
+// profiles/r05/r05t_place_micro.txt; the same pass into two such buffers: 1.46
+// vs 1.76 ms).  A large row buffer is therefore probed when it is allocated
+// (hj::placement_probe: the pass's pattern against a flat write, ~2 ms) and
+// redrawn while it is slow: up to kPlaceDraws allocations, the rejected ones
+// held until the choice is made (so the allocator cannot hand them back) and
+// then freed; the best draw is kept.  HJ_PLACEMENT_PROBE=0 turns it off.
+constexpr size_t kPlaceMinBytes = size_t(1) << 32;   // smaller sets: every draw measured alike (r05t)
+constexpr int kPlaceDraws = 12;
+constexpr float kPlaceGood = 1.12f;                  // pattern / flat at a good placement: 0.98-1.05
+struct PlaceStats {
+    long long probes = 0, rejected = 0;
+    double worst_kept = 0.0, last_kept = 0.0;
+};
+PlaceStats g_place;
+std::mutex g_place_mu;
+
+bool placement_probe_on() {
+    static const bool on = [] {
+        const char *e = getenv("HJ_PLACEMENT_PROBE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+int ensure_rows(Buf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.bytes >= bytes) return HJ_OK;
+    if (bytes < kPlaceMinBytes || !placement_probe_on()) return ensure_buf(b, bytes);
+    free_buf(b);
+    int dev = 0, cus = 0;
+    HJ_HIP(hipGetDevice(&dev));
+    HJ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<Buf> rejected;
+    Buf best;
+    float best_r = 1e30f;
+    int draws = 0;
+    for (; draws < kPlaceDraws; ++draws) {
+        if (draws > 0) {
+            // another draw only with room for it and twice its size to spare
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < 3 * bytes) break;
+        }
+        Buf cand;
+        if (hipMalloc(&cand.p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            break;
+        }
+        cand.bytes = bytes;
+        float r = 0.0f;
+        if (hj::placement_probe(cand.p, bytes, cus, &r) != hipSuccess) {
+            (void)hipGetLastError();
+            r = 0.0f;   // no verdict: take it
+        }
+        if (r < best_r) {
+            if (best.p) rejected.push_back(best);
+            best = cand;
+            best_r = r;
+        } else {
+            rejected.push_back(cand);
+        }
+        if (best_r <= kPlaceGood) {
+            ++draws;
+            break;
+        }
+    }
+    for (Buf &x : rejected) free_buf(x);
+    if (!best.p) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc radix rows " + std::to_string(bytes));
+    b = best;
+    {
+        std::lock_guard<std::mutex> lk(g_place_mu);
+        g_place.probes += draws;
+        g_place.rejected += (long long)rejected.size();
+        g_place.last_kept = best_r;
+        if (best_r > g_place.worst_kept) g_place.worst_kept = best_r;
+    }
+    if (trace_on())
+        std::fprintf(stderr, "hj trace: rows placement %zu B: %d draw(s), kept pattern/flat %.3f\n", bytes, draws,
+                     (double)best_r);
+    return HJ_OK;
+}
+
 int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
     if (need.buckets > 0xFFFFFFF0ull) HJ_FAIL(HJ_ERR_CAPACITY, "radix partition: too many buckets");
-    HJ_TRY(ensure_buf(sb.rows, (size_t)need.rows * esz));
+    HJ_TRY(ensure_rows(sb.rows, (size_t)need.rows * esz));
     HJ_TRY(ensure_buf(sb.bbin, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.bfill, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.rstart, (P + 1) * 8));
@@ -1763,3 +1849,11 @@ int64_t hj_select_f32(float *, float *in, int64_t in_off, int64_t in_size, int64
 void hj_free_result(void *allocated) { std::free(allocated); }
 
 }  // extern "C"
+
+void hj_placement_stats(long long *probes, long long *rejected, double *last_kept, double *worst_kept) {
+    std::lock_guard<std::mutex> lk(g_place_mu);
+    if (probes) *probes = g_place.probes;
+    if (rejected) *rejected = g_place.rejected;
+    if (last_kept) *last_kept = g_place.last_kept;
+    if (worst_kept) *worst_kept = g_place.worst_kept;
+}

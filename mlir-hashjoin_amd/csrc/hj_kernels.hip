@@ -1122,4 +1122,69 @@ hipError_t launch_stream_copy(const void *in, void *out, long long rows, int sha
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- placement probe
+// The partition passes write, per 4096-row tile, one 128-B line into each of
+// ~512 open 1024-row buckets of the workgroup's own bucket range.  Into some
+// physical placements of the destination buffer that pattern runs 25-35 %
+// slower than a flat write of the same bytes; it is a property of the
+// allocation (bimodal, reproducible per buffer, the flat write and flat read
+// never vary, contiguous allocations are slow more often:
+// profiles/r05/r05t_place_micro.txt, r05u_*).  placement_probe writes the
+// pass's pattern (synthetic rows, every workgroup in its own range) and a flat
+// stream of the same bytes into a fresh buffer; ratio = pattern / flat.
+__global__ __launch_bounds__(1024) void k_place_pattern(cp_v2 *__restrict__ out, unsigned tpw, cp_u64 wrows) {
+    const unsigned w = blockIdx.x, tid = threadIdx.x;
+    const cp_u64 base = (cp_u64)w * wrows;
+    const cp_v2 val = {(cp_u64)w, 1ull};
+    for (unsigned t = 0; t < tpw; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const unsigned j = (unsigned)i * 128u + (tid >> 3);   // the line's bin
+            cp_st(out + base + ((cp_u64)(t >> 7) * 512u + j) * 1024u + (t & 127u) * 8u + (tid & 7u), val);
+        }
+}
+
+__global__ __launch_bounds__(256) void k_place_flat(cp_v2 *__restrict__ out, cp_u64 n) {
+    const cp_u64 i = (cp_u64)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) cp_st(out + i, cp_v2{i, 2ull});
+}
+
+hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio) {
+    *ratio = 0.0f;
+    if (cus <= 0 || !buf) return hipErrorInvalidValue;
+    // every workgroup's range: whole 1024-row buckets, >= two per bin (512 bins)
+    const cp_u64 wrows = ((cp_u64)(bytes / 16) / (cp_u64)cus) & ~(cp_u64)1023;
+    const cp_u64 buckets = wrows / 1024;
+    if (buckets < 1024) return hipErrorInvalidValue;
+    // tiles per workgroup: a bin's buckets (t >> 7) stay inside the range
+    const unsigned tpw = (unsigned)((buckets / 512 - 1) * 128 > 512 ? 512 : (buckets / 512 - 1) * 128);
+    const cp_u64 flat = (cp_u64)tpw * 4096u * (cp_u64)cus;   // the same rows, streamed
+    cp_v2 *out = (cp_v2 *)buf;
+    hipEvent_t e[4];
+    hipError_t err = hipSuccess;
+    int made = 0;
+    for (; made < 4 && err == hipSuccess; ++made) err = hipEventCreate(&e[made]);
+    float best_p = 1e30f, best_f = 1e30f;
+    for (int rep = 0; rep < 3 && err == hipSuccess; ++rep) {
+        // rep 0 warms up (first touch of the pages), reps 1-2 are kept
+        err = hipEventRecord(e[0], 0);
+        hipLaunchKernelGGL(k_place_pattern, dim3(cus), dim3(1024), 0, 0, out, tpw, wrows);
+        if (err == hipSuccess) err = hipEventRecord(e[1], 0);
+        hipLaunchKernelGGL(k_place_flat, dim3((unsigned)((flat + 255) / 256)), dim3(256), 0, 0, out, flat);
+        if (err == hipSuccess) err = hipEventRecord(e[2], 0);
+        if (err == hipSuccess) err = hipGetLastError();
+        if (err == hipSuccess) err = hipEventSynchronize(e[2]);
+        float tp = 0.0f, tf = 0.0f;
+        if (err == hipSuccess) err = hipEventElapsedTime(&tp, e[0], e[1]);
+        if (err == hipSuccess) err = hipEventElapsedTime(&tf, e[1], e[2]);
+        if (rep > 0 && err == hipSuccess) {
+            if (tp < best_p) best_p = tp;
+            if (tf < best_f) best_f = tf;
+        }
+    }
+    for (int i = 0; i < made; ++i) (void)hipEventDestroy(e[i]);
+    if (err == hipSuccess) *ratio = best_f > 0.0f ? best_p / best_f : 0.0f;
+    return err;
+}
+
 }  // namespace hj

@@ -7,7 +7,7 @@ missing: there is no CPU fallback.
 """
 from ._lib import HJError, check, declared_symbols, lib  # noqa: F401
 from .join import (HashJoin, device_info, gen_pkfk, gen_uniform_i32, gen_uniform_i64, gen_zipf,  # noqa: F401
-                   hit_threshold, partition_of, stream_copy, zipf_params)
+                   hit_threshold, partition_of, placement_stats, stream_copy, zipf_params)
 
 __all__ = ["HashJoin", "device_info", "HJError", "gen_pkfk", "gen_uniform_i32", "gen_uniform_i64", "hit_threshold",
-           "partition_of", "stream_copy", "gen_zipf", "zipf_params", "lib", "check", "declared_symbols"]
+           "partition_of", "placement_stats", "stream_copy", "gen_zipf", "zipf_params", "lib", "check", "declared_symbols"]

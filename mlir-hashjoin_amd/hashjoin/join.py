@@ -407,6 +407,17 @@ def stream_copy(src, dst, shape="persistent", stream=None):
           "hj_dev_stream_copy")
 
 
+def placement_stats():
+    """Row-buffer placement probe counts of this process (hj_placement_stats):
+    draws probed / rejected and the pattern/flat write ratio of the last and
+    the worst buffer kept (~1.0 good, 1.25-1.35 a slow placement)."""
+    pr, rj = C.c_longlong(0), C.c_longlong(0)
+    last, worst = C.c_double(0.0), C.c_double(0.0)
+    lib.hj_placement_stats(C.byref(pr), C.byref(rj), C.byref(last), C.byref(worst))
+    return {"probes": pr.value, "rejected": rj.value, "last_kept_ratio": round(last.value, 3),
+            "worst_kept_ratio": round(worst.value, 3)}
+
+
 def partition_of(key: int, nparts: int) -> int:
     """Owner of a key under the routing hash (host function of libhj.so)."""
     return int(lib.hj_partition_of(int(key), int(nparts)))
