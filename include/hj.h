@@ -262,7 +262,7 @@ int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_
 int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void *stream);
 
 /* Placement of the radix bucket sets' row buffers (diagnostics, no reference
- * counterpart).  A row buffer of >= 4 GiB is probed when allocated: the
+ * counterpart).  A row buffer of >= 1 GiB is probed when allocated: the
  * partition pass's write pattern against a flat write of the same bytes
  * (some physical placements run the pattern 25-35 % slower), redrawn up to 12
  * times while slow, best draw kept; HJ_PLACEMENT_PROBE=0 in the environment

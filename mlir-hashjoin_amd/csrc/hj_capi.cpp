@@ -278,7 +278,7 @@ void free_buf(Buf &b) {
 // redrawn while it is slow: up to kPlaceDraws allocations, the rejected ones
 // held until the choice is made (so the allocator cannot hand them back) and
 // then freed; the best draw is kept.  HJ_PLACEMENT_PROBE=0 turns it off.
-constexpr size_t kPlaceMinBytes = size_t(1) << 32;   // smaller sets: every draw measured alike (r05t)
+constexpr size_t kPlaceMinBytes = size_t(1) << 30;   // (the probe needs >= 4 MiB per CU)
 constexpr int kPlaceDraws = 12;
 constexpr float kPlaceGood = 1.12f;                  // pattern / flat at a good placement: 0.98-1.05
 struct PlaceStats {

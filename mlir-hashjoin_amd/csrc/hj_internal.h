@@ -258,7 +258,7 @@ hipError_t launch_select_i64(const long long *in, long long n, int op, long long
 // copy floors (hj_dev_stream_copy): shape 0 persistent (cus workgroups), 1 flat
 hipError_t launch_stream_copy(const void *in, void *out, long long rows, int shape, int cus, hipStream_t st);
 // the partition pass's write pattern vs a flat write of the same bytes into a
-// fresh buffer (>= cus x 16 MiB): *ratio = pattern time / flat time, ~1.0 at
+// fresh buffer (>= cus x 4 MiB): *ratio = pattern time / flat time, ~1.0 at
 // a good physical placement, 1.25-1.35 at a bad one (hj_kernels.hip)
 hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio);
 

@@ -1132,15 +1132,17 @@ hipError_t launch_stream_copy(const void *in, void *out, long long rows, int sha
 // profiles/r05/r05t_place_micro.txt, r05u_*).  placement_probe writes the
 // pass's pattern (synthetic rows, every workgroup in its own range) and a flat
 // stream of the same bytes into a fresh buffer; ratio = pattern / flat.
-__global__ __launch_bounds__(1024) void k_place_pattern(cp_v2 *__restrict__ out, unsigned tpw, cp_u64 wrows) {
+// (nb = 128 / 256 / 512 open buckets per workgroup: nb / 128 lines per
+// thread group of 8 lanes per tile)
+__global__ __launch_bounds__(1024) void k_place_pattern(cp_v2 *__restrict__ out, unsigned tpw, cp_u64 wrows,
+                                                        unsigned nb) {
     const unsigned w = blockIdx.x, tid = threadIdx.x;
     const cp_u64 base = (cp_u64)w * wrows;
     const cp_v2 val = {(cp_u64)w, 1ull};
     for (unsigned t = 0; t < tpw; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const unsigned j = (unsigned)i * 128u + (tid >> 3);   // the line's bin
-            cp_st(out + base + ((cp_u64)(t >> 7) * 512u + j) * 1024u + (t & 127u) * 8u + (tid & 7u), val);
+        for (unsigned i = 0; i < nb / 128u; ++i) {
+            const unsigned j = i * 128u + (tid >> 3);   // the line's bin
+            cp_st(out + base + ((cp_u64)(t >> 7) * nb + j) * 1024u + (t & 127u) * 8u + (tid & 7u), val);
         }
 }
 
@@ -1152,13 +1154,16 @@ __global__ __launch_bounds__(256) void k_place_flat(cp_v2 *__restrict__ out, cp_
 hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio) {
     *ratio = 0.0f;
     if (cus <= 0 || !buf) return hipErrorInvalidValue;
-    // every workgroup's range: whole 1024-row buckets, >= two per bin (512 bins)
+    // every workgroup's range: whole 1024-row buckets, >= two per bin (512
+    // bins; 256 / 128 in smaller buffers)
     const cp_u64 wrows = ((cp_u64)(bytes / 16) / (cp_u64)cus) & ~(cp_u64)1023;
     const cp_u64 buckets = wrows / 1024;
-    if (buckets < 1024) return hipErrorInvalidValue;
+    const unsigned nb = buckets >= 1024 ? 512u : buckets >= 512 ? 256u : 128u;
+    if (buckets < 256) return hipErrorInvalidValue;
     // tiles per workgroup: a bin's buckets (t >> 7) stay inside the range
-    const unsigned tpw = (unsigned)((buckets / 512 - 1) * 128 > 512 ? 512 : (buckets / 512 - 1) * 128);
-    const cp_u64 flat = (cp_u64)tpw * 4096u * (cp_u64)cus;   // the same rows, streamed
+    const cp_u64 tw = (buckets / nb - 1) * 128;
+    const unsigned tpw = (unsigned)(tw > 512 ? 512 : tw);
+    const cp_u64 flat = (cp_u64)tpw * 8u * nb * (cp_u64)cus;   // the same rows, streamed
     cp_v2 *out = (cp_v2 *)buf;
     hipEvent_t e[4];
     hipError_t err = hipSuccess;
@@ -1168,7 +1173,7 @@ hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio) {
     for (int rep = 0; rep < 3 && err == hipSuccess; ++rep) {
         // rep 0 warms up (first touch of the pages), reps 1-2 are kept
         err = hipEventRecord(e[0], 0);
-        hipLaunchKernelGGL(k_place_pattern, dim3(cus), dim3(1024), 0, 0, out, tpw, wrows);
+        hipLaunchKernelGGL(k_place_pattern, dim3(cus), dim3(1024), 0, 0, out, tpw, wrows, nb);
         if (err == hipSuccess) err = hipEventRecord(e[1], 0);
         hipLaunchKernelGGL(k_place_flat, dim3((unsigned)((flat + 255) / 256)), dim3(256), 0, 0, out, flat);
         if (err == hipSuccess) err = hipEventRecord(e[2], 0);

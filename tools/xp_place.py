@@ -1,7 +1,7 @@
 """Placement probe A/B: C3 build + probe on ten fresh contexts in one process
 (each context allocates new bucket sets), phase times per context and the
 probe's counts.  Run once with HJ_PLACEMENT_PROBE=0 and once without.
-    python tools/xp_place.py [contexts] > out.jsonl
+    python tools/xp_place.py [contexts] [config] > out.jsonl
 """
 import json
 import os
@@ -41,7 +41,8 @@ def run(rk, rp, sk, sp, steps=5):
 
 def main():
     nctx = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    NR, NS, distn, _, _ = bench.CONFIGS["C3"]
+    cfg = sys.argv[2] if len(sys.argv) > 2 else "C3"
+    NR, NS, distn, _, _ = bench.CONFIGS[cfg]
 
     class A:
         seed = 42
@@ -50,6 +51,7 @@ def main():
     for k in range(nctx):
         r = run(rk, rp, sk, sp)
         r["ctx"] = k
+        r["config"] = cfg
         r["placement"] = hashjoin.placement_stats()
         r["probe_env"] = os.environ.get("HJ_PLACEMENT_PROBE", "1")
         print(json.dumps(r), flush=True)
