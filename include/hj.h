@@ -262,7 +262,7 @@ int hj_dev_select_i64(hj_ctx *ctx, const int64_t *in, int64_t n, int cmp, int64_
 int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void *stream);
 
 /* Placement of the radix bucket sets' row buffers (diagnostics, no reference
- * counterpart).  A row buffer of >= 1 GiB is probed when allocated: the
+ * counterpart).  A row buffer of >= 1 GiB (buckets >= 8 KiB) is probed when allocated: the
  * partition pass's write pattern against a flat write of the same bytes
  * (some physical placements run the pattern 25-35 % slower), redrawn up to 12
  * times while slow, best draw kept; HJ_PLACEMENT_PROBE=0 in the environment
@@ -270,6 +270,12 @@ int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void 
  * rejected, and the pattern/flat ratio of the last and of the worst kept
  * buffer (0 when none was probed).  Any pointer may be null. */
 void hj_placement_stats(long long *probes, long long *rejected, double *last_kept, double *worst_kept);
+/* The same probe on a caller's device buffer of >= 4 MiB per CU (its
+ * contents are overwritten): *ratio = pass-pattern time / flat-write time
+ * (~1.0 good placement, 1.25-1.35 slow).  Synchronous on the default stream.
+ * The Python host side draws the routed-tuple buffers of hj_dev_route_i64
+ * with it (hashjoin.HashJoin.route). */
+int hj_placement_check(const void *buf, int64_t bytes, double *ratio);
 
 /* Out-of-core join of HOST-resident int64 key/payload columns (relations
  * larger than HBM; the reference leaves the partitioned join out,

@@ -278,7 +278,11 @@ void free_buf(Buf &b) {
 // redrawn while it is slow: up to kPlaceDraws allocations, the rejected ones
 // held until the choice is made (so the allocator cannot hand them back) and
 // then freed; the best draw is kept.  HJ_PLACEMENT_PROBE=0 turns it off.
-constexpr size_t kPlaceMinBytes = size_t(1) << 30;   // (the probe needs >= 4 MiB per CU)
+// (smaller buffers, and 4-KiB buckets (i32 rows' final sets), probe too short
+// a pattern to judge: REF-B's sets were rejected 9 draws in 10 at unchanged
+// pass times, profiles/r05/r05y_*)
+constexpr size_t kPlaceMinBytes = size_t(1) << 30;
+constexpr size_t kPlaceMinBucket = size_t(8) << 10;
 constexpr int kPlaceDraws = 12;
 constexpr float kPlaceGood = 1.12f;                  // pattern / flat at a good placement: 0.98-1.05
 struct PlaceStats {
@@ -296,10 +300,10 @@ bool placement_probe_on() {
     return on;
 }
 
-int ensure_rows(Buf &b, size_t bytes) {
+int ensure_rows(Buf &b, size_t bytes, size_t bucket_bytes) {
     if (bytes == 0) bytes = 16;
     if (b.bytes >= bytes) return HJ_OK;
-    if (bytes < kPlaceMinBytes || !placement_probe_on()) return ensure_buf(b, bytes);
+    if (bytes < kPlaceMinBytes || bucket_bytes < kPlaceMinBucket || !placement_probe_on()) return ensure_buf(b, bytes);
     free_buf(b);
     int dev = 0, cus = 0;
     HJ_HIP(hipGetDevice(&dev));
@@ -321,7 +325,7 @@ int ensure_rows(Buf &b, size_t bytes) {
         }
         cand.bytes = bytes;
         float r = 0.0f;
-        if (hj::placement_probe(cand.p, bytes, cus, &r) != hipSuccess) {
+        if (hj::placement_probe(cand.p, bytes, bucket_bytes, cus, &r) != hipSuccess) {
             (void)hipGetLastError();
             r = 0.0f;   // no verdict: take it
         }
@@ -353,9 +357,9 @@ int ensure_rows(Buf &b, size_t bytes) {
     return HJ_OK;
 }
 
-int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P) {
+int ensure_set(SetBufs &sb, const hj::RadixNeed &need, size_t esz, size_t P, int pbl) {
     if (need.buckets > 0xFFFFFFF0ull) HJ_FAIL(HJ_ERR_CAPACITY, "radix partition: too many buckets");
-    HJ_TRY(ensure_rows(sb.rows, (size_t)need.rows * esz));
+    HJ_TRY(ensure_rows(sb.rows, (size_t)need.rows * esz, esz << pbl));
     HJ_TRY(ensure_buf(sb.bbin, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.bfill, (size_t)need.buckets * 4));
     HJ_TRY(ensure_buf(sb.rstart, (P + 1) * 8));
@@ -387,8 +391,8 @@ hj::BucketSet bucket_set(SetBufs &sb) {
 // relation's own final set.
 int ensure_radix_scratch(hj_ctx *c, SetBufs &fin, int64_t n, size_t esz, const hj::RadixPlan &pl) {
     const size_t P = size_t(1) << pl.total_bits;
-    HJ_TRY(ensure_set(fin, hj::radix_need(n, pl, true), esz, P));
-    if (pl.passes > 1) HJ_TRY(ensure_set(c->tset, hj::radix_need(n, pl, false), esz, P));
+    HJ_TRY(ensure_set(fin, hj::radix_need(n, pl, true), esz, P, hj::kFinalPbl));
+    if (pl.passes > 1) HJ_TRY(ensure_set(c->tset, hj::radix_need(n, pl, false), esz, P, hj::kPassPbl));
     HJ_TRY(ensure_buf(c->nb, 16));
     HJ_TRY(ensure_buf(c->pcur, (P + 1) * 8));
     HJ_TRY(ensure_buf(c->rcur, (P + 1) * 8));
@@ -1856,4 +1860,18 @@ void hj_placement_stats(long long *probes, long long *rejected, double *last_kep
     if (rejected) *rejected = g_place.rejected;
     if (last_kept) *last_kept = g_place.last_kept;
     if (worst_kept) *worst_kept = g_place.worst_kept;
+}
+
+int hj_placement_check(const void *buf, int64_t bytes, double *ratio) {
+    if (!buf || bytes <= 0 || !ratio) HJ_FAIL(HJ_ERR_ARG, "placement check: null buffer / ratio or no bytes");
+    *ratio = 0.0;
+    int dev = 0, cus = 0;
+    HJ_HIP(hipGetDevice(&dev));
+    HJ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    float r = 0.0f;
+    const hipError_t e = hj::placement_probe(const_cast<void *>(buf), (size_t)bytes, size_t(16) << hj::kPassPbl, cus, &r);
+    if (e == hipErrorInvalidValue) HJ_FAIL(HJ_ERR_ARG, "placement check: buffer below 4 MiB per CU");
+    HJ_HIP(e);
+    *ratio = r;
+    return HJ_OK;
 }

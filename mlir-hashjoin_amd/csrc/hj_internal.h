@@ -143,6 +143,7 @@ constexpr int kRunLog = 6;
 // readable entries past max_runs in a run list: the joins load a wave's
 // entries in one scalar load of up to 4, past the list's end included
 constexpr int kRunPad = 8;
+constexpr int kPassPbl = 10;   // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
 constexpr int kFinalPbl = 9;   // 512-row buckets for the join's input (8 / 9 / 10+9 measured: profiles/r01_bucket_sizes.txt)
 struct BucketSet {
     void *rows;                    // >= max_buckets << pbl rows
@@ -257,10 +258,11 @@ hipError_t launch_select_i64(const long long *in, long long n, int op, long long
                              unsigned long long *sums, hipStream_t st);
 // copy floors (hj_dev_stream_copy): shape 0 persistent (cus workgroups), 1 flat
 hipError_t launch_stream_copy(const void *in, void *out, long long rows, int shape, int cus, hipStream_t st);
-// the partition pass's write pattern vs a flat write of the same bytes into a
-// fresh buffer (>= cus x 4 MiB): *ratio = pattern time / flat time, ~1.0 at
-// a good physical placement, 1.25-1.35 at a bad one (hj_kernels.hip)
-hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio);
+// the partition pass's write pattern (buckets of bucket_bytes: 4-16 KiB) vs a
+// flat write of the same bytes into a fresh buffer (>= cus x 256 buckets):
+// *ratio = pattern time / flat time, ~1.0 at a good physical placement,
+// 1.25-1.35 at a bad one (hj_kernels.hip)
+hipError_t placement_probe(void *buf, size_t bytes, size_t bucket_bytes, int cus, float *ratio);
 
 // nested-loop.mlir result rows (hj_kernels.hip)
 hipError_t launch_key_col_i32(const int *t, long long rows, long long ld, int *out, hipStream_t st);

@@ -1133,16 +1133,17 @@ hipError_t launch_stream_copy(const void *in, void *out, long long rows, int sha
 // pass's pattern (synthetic rows, every workgroup in its own range) and a flat
 // stream of the same bytes into a fresh buffer; ratio = pattern / flat.
 // (nb = 128 / 256 / 512 open buckets per workgroup: nb / 128 lines per
-// thread group of 8 lanes per tile)
+// thread group of 8 lanes per tile; buckets of 2^lpb_log 128-B lines)
 __global__ __launch_bounds__(1024) void k_place_pattern(cp_v2 *__restrict__ out, unsigned tpw, cp_u64 wrows,
-                                                        unsigned nb) {
+                                                        unsigned nb, unsigned lpb_log) {
     const unsigned w = blockIdx.x, tid = threadIdx.x;
     const cp_u64 base = (cp_u64)w * wrows;
     const cp_v2 val = {(cp_u64)w, 1ull};
+    const unsigned lmask = (1u << lpb_log) - 1u;
     for (unsigned t = 0; t < tpw; ++t)
         for (unsigned i = 0; i < nb / 128u; ++i) {
             const unsigned j = i * 128u + (tid >> 3);   // the line's bin
-            cp_st(out + base + ((cp_u64)(t >> 7) * nb + j) * 1024u + (t & 127u) * 8u + (tid & 7u), val);
+            cp_st(out + base + ((((cp_u64)(t >> lpb_log) * nb + j) << lpb_log) + (t & lmask)) * 8u + (tid & 7u), val);
         }
 }
 
@@ -1151,17 +1152,21 @@ __global__ __launch_bounds__(256) void k_place_flat(cp_v2 *__restrict__ out, cp_
     if (i < n) cp_st(out + i, cp_v2{i, 2ull});
 }
 
-hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio) {
+hipError_t placement_probe(void *buf, size_t bytes, size_t bucket_bytes, int cus, float *ratio) {
     *ratio = 0.0f;
     if (cus <= 0 || !buf) return hipErrorInvalidValue;
-    // every workgroup's range: whole 1024-row buckets, >= two per bin (512
-    // bins; 256 / 128 in smaller buffers)
-    const cp_u64 wrows = ((cp_u64)(bytes / 16) / (cp_u64)cus) & ~(cp_u64)1023;
-    const cp_u64 buckets = wrows / 1024;
+    // 128-B lines per bucket (a power of two, 8 .. 128)
+    unsigned lpb_log = 3;
+    while (lpb_log < 7 && (size_t(128) << (lpb_log + 1)) <= bucket_bytes) ++lpb_log;
+    const cp_u64 bv2 = (cp_u64)8 << lpb_log;   // 16-B units per bucket
+    // every workgroup's range: whole buckets, >= two per bin (512 bins; 256 /
+    // 128 in smaller buffers)
+    const cp_u64 wrows = ((cp_u64)(bytes / 16) / (cp_u64)cus) / bv2 * bv2;
+    const cp_u64 buckets = wrows / bv2;
     const unsigned nb = buckets >= 1024 ? 512u : buckets >= 512 ? 256u : 128u;
     if (buckets < 256) return hipErrorInvalidValue;
-    // tiles per workgroup: a bin's buckets (t >> 7) stay inside the range
-    const cp_u64 tw = (buckets / nb - 1) * 128;
+    // tiles per workgroup: a bin's buckets (t >> lpb_log) stay inside the range
+    const cp_u64 tw = (buckets / nb - 1) << lpb_log;
     const unsigned tpw = (unsigned)(tw > 512 ? 512 : tw);
     const cp_u64 flat = (cp_u64)tpw * 8u * nb * (cp_u64)cus;   // the same rows, streamed
     cp_v2 *out = (cp_v2 *)buf;
@@ -1173,7 +1178,7 @@ hipError_t placement_probe(void *buf, size_t bytes, int cus, float *ratio) {
     for (int rep = 0; rep < 3 && err == hipSuccess; ++rep) {
         // rep 0 warms up (first touch of the pages), reps 1-2 are kept
         err = hipEventRecord(e[0], 0);
-        hipLaunchKernelGGL(k_place_pattern, dim3(cus), dim3(1024), 0, 0, out, tpw, wrows, nb);
+        hipLaunchKernelGGL(k_place_pattern, dim3(cus), dim3(1024), 0, 0, out, tpw, wrows, nb, lpb_log);
         if (err == hipSuccess) err = hipEventRecord(e[1], 0);
         hipLaunchKernelGGL(k_place_flat, dim3((unsigned)((flat + 255) / 256)), dim3(256), 0, 0, out, flat);
         if (err == hipSuccess) err = hipEventRecord(e[2], 0);

@@ -59,7 +59,6 @@ constexpr unsigned kNoBucket = 0xFFFFFFFFu;
 // Join items of multi-chunk partitions first (k_item_desc): int64 rows only
 // (profiles/r03_heavy_first.txt).
 constexpr bool kHeavyFirst = true;
-constexpr int kPassPbl = 10;       // 1024-row buckets for intermediate passes (9: 1 % slower C3 step)
 
 __device__ __forceinline__ u64 rhash(u64 k) { return radix_hash(k); }
 
@@ -2245,14 +2244,23 @@ __global__ __launch_bounds__(NT, WPS) void k_join_u(JoinArgs a) {
 // keys in [1, 100k]) goes to k_join_grp before anything of it is written.
 // the int64 rows' fast join shape (see "join shapes" below)
 constexpr int kFastNTc = 768, kFastRIc = 3, kFastSIc = 3, kFastWPSc = 6;
+#ifndef HJ_WIDE_DYN
+#define HJ_WIDE_DYN 1   // int64 rows claim items from a counter (0: static w += grid, for A/B)
+#endif
 
 template <bool WIDE, int NT, int SI, bool DETECT, int TSL>
 struct JoinBSmem {
     static constexpr int TS = 1 << TSL, NB = TS / 4, NW = NT / 64;
     static constexpr unsigned kSusCap = 512;
+    // int64 rows: bucket words and control words double-buffered (an item
+    // clears the next item's set: no clear barrier); i32 rows' 64-KiB table
+    // leaves no room for a second set at two workgroups per CU
+    static constexpr bool DBL = WIDE && !DETECT;
     alignas(16) u64 tkey[TS];
     alignas(16) u64 tpay[WIDE ? TS : 2];
     alignas(16) unsigned bcnt[NB];
+    alignas(16) unsigned bcnt2[DBL ? NB : 4];
+    alignas(16) unsigned s_ctl2[4];
     alignas(16) unsigned bsig[DETECT ? NB : 4];
     unsigned sus[DETECT ? kSusCap : 1];
     u64 s_base;
@@ -2284,26 +2292,30 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
     constexpr unsigned kCntMask = 0xFFFFu;
     auto &tkey = sm.tkey;
     auto &tpay = sm.tpay;
-    auto &bcnt = sm.bcnt;
+    unsigned *bcnt = sm.bcnt;   // this item's bucket words (DBL: flips per table built)
     // (DETECT) per home bucket the OR of its rows' 1-of-32 key signatures,
     // and the suspect slots: slot | home bucket << 16
     constexpr unsigned kSusCap = JoinBSmem<WIDE, NT, SI, DETECT, TSL>::kSusCap;
     auto &bsig = sm.bsig;
     auto &sus = sm.sus;
     auto &s_base = sm.s_base;
-    auto &s_ctl = sm.s_ctl;   // s_bad, s_dup, s_rows, s_nsus (one 16-B clear)
-    unsigned &s_bad = s_ctl[0], &s_dup = s_ctl[1], &s_rows = s_ctl[2], &s_nsus = s_ctl[3];
+    // [0] bad (defer the item), [1] dup (a repeated build key met), [2] rows
+    // in the table, [3] suspects (DETECT): one 16-B clear; DBL: flips with bcnt
+    unsigned *s_ctl = sm.s_ctl;
+    constexpr bool DBL = JoinBSmem<WIDE, NT, SI, DETECT, TSL>::DBL;
     // per (row slot, wave) ballot counts, then per wave the multi rows' pairs
     auto &s_cw = sm.s_cw;
     auto &s_skip = sm.s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
     auto &s_mpre = sm.s_mpre;   // a thread's multi pairs before it in its wave (kept out of registers)
-    // a.next_item (i32 rows; int64 rows and DETECT walk w += grid: the wide
-    // instantiation has no SGPRs left for it, its next item's run entries
-    // already fill them -- with the claim it spilled 20 B and lost 6 % on C3
-    // while C4 gained 5 %, profiles/r03_narrow_shapes.txt 6): iteration k claims the
-    // item of iteration k + 2 into s_next after its first barrier, and the top
-    // of iteration k + 1 reads it (a workgroup's first two items are static:
-    // blockIdx.x, blockIdx.x + grid)
+    // a.next_item (DETECT walks w += grid): iteration k claims the item of
+    // iteration k + 2 into s_next after its first barrier (DBL: after the
+    // build barrier, the first one it has), and the top of iteration k + 1
+    // reads it (a workgroup's first two items are static: blockIdx.x,
+    // blockIdx.x + grid).  int64 rows claim since round 5: the double-buffered
+    // words took the clear barrier and 4 VGPRs off the kernel, and the claim
+    // no longer spills (round 3: 20 B, C3 -6 %); C3 join 2.46 -> 2.30 ms, C4
+    // 2.82 -> 2.45 (profiles/r05/r05y_wdyn_alt.jsonl: skewed items no longer
+    // pile up on the workgroups a static stride gave them to)
     auto &s_next = sm.s_next;
     bool dup_sent = false;
 
@@ -2391,9 +2403,16 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
     unsigned nvr = ents(a.r_runs, it.r_lo, it.r_hi, er, RI), nvs = 0;
     // (DETECT reads no probe rows)
     if (!DETECT) nvs = ents(a.s_runs, it.s_lo, it.s_lo + subb < it.s_hi ? it.s_lo + subb : it.s_hi, es, SI);
-    constexpr bool dyn = !DETECT && !WIDE;
+    constexpr bool dyn = !DETECT && (!WIDE || HJ_WIDE_DYN);
     if (dyn) {
         if (threadIdx.x == 0) s_next = w + gridDim.x;
+        __syncthreads();
+    }
+    if constexpr (DBL) {
+        // the first table's words (each later table's are cleared by the item
+        // before it)
+        for (unsigned j = threadIdx.x; j < (unsigned)NB; j += NT) bcnt[j] = 0u;
+        if (threadIdx.x < 4) s_ctl[threadIdx.x] = 0u;
         __syncthreads();
     }
     while (true) {
@@ -2428,17 +2447,26 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
             const unsigned z = (unsigned)(it.r_lo >> 63);
             const uint4 z4 = make_uint4(z, z, z, z);
             // (thread 0 clears the control words: it is also the one that
-            // reads the previous item's s_dup after the item's last barrier)
+            // reads the previous item's dup word after the item's last barrier)
             static_assert(NB / 4 <= NT, "one 16-B clear per thread: bucket words");
             // (the index carries z too: a loop-invariant clear address was
             // hoisted out of the item loop and spilled)
             const unsigned ci = threadIdx.x + z;
-            if (ci < NB / 4) ((uint4 *)bcnt)[ci] = z4;
-            if (DETECT)
-                for (unsigned j = ci; j < NB / 4; j += NT) ((uint4 *)bsig)[j] = z4;
-            if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
-            __syncthreads();
-            if (dyn && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
+            if constexpr (DBL) {
+                // the NEXT table's words (this one's were cleared by the item
+                // before, or before the loop): no barrier here
+                unsigned *const nb_ = bcnt == sm.bcnt ? sm.bcnt2 : sm.bcnt;
+                if (ci < NB / 4) ((uint4 *)nb_)[ci] = z4;
+                if (threadIdx.x == 0) *(uint4 *)(s_ctl == sm.s_ctl ? sm.s_ctl2 : sm.s_ctl) = z4;
+            } else {
+                if (ci < NB / 4) ((uint4 *)bcnt)[ci] = z4;
+                if (DETECT)
+                    for (unsigned j = ci; j < NB / 4; j += NT) ((uint4 *)bsig)[j] = z4;
+                if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
+                __syncthreads();
+            }
+            // (DBL: no barrier above -- the claim waits for the build barrier)
+            if (dyn && !DBL && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
             // ---- build: every row's rank add issued before any is used
             bool bad = false;
             for (u64 r0 = it.r_lo;;) {
@@ -2464,7 +2492,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                     unsigned wn = 0;
 #pragma unroll
                     for (int i = 0; i < RI; ++i) wn += (unsigned)__popcll(__ballot((rok >> i) & 1u));
-                    if (lane == 0 && wn && atomicAdd(&s_rows, wn) + wn > rmax_rows) s_bad = 1u;
+                    if (lane == 0 && wn && atomicAdd(&s_ctl[2], wn) + wn > rmax_rows) s_ctl[0] = 1u;
                 }
 #pragma unroll
                 for (int i = 0; i < RI; ++i) {
@@ -2482,7 +2510,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                         rk[i] = atomicAdd(&bcnt[bb[i]], 1u) & kCntMask;
                     }
                     if (rk[i] >= (unsigned)BW) {   // (only past rmax_rows: deferred)
-                        s_bad = 1u;
+                        s_ctl[0] = 1u;
                         continue;
                     }
                     const unsigned slot = bb[i] * BW + rk[i];
@@ -2494,7 +2522,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                         tidn[slot] = (unsigned)R::pay(rv_[i]);
                     }
                     if (DETECT && ((susm >> i) & 1u)) {
-                        const unsigned q = atomicAdd(&s_nsus, 1u);
+                        const unsigned q = atomicAdd(&s_ctl[3], 1u);
                         if (q < kSusCap) sus[q] = slot | home << 16;
                     }
                 }
@@ -2503,9 +2531,10 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                 nvr = ents(a.r_runs, r0, it.r_hi, er, RI);
                 rok = rows_of(rrows, er, nvr, rv_, RI);
             }
-            if (bad) s_bad = 1u;
+            if (bad) s_ctl[0] = 1u;
             __syncthreads();
-            if (s_bad) {
+            if (dyn && DBL && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
+            if (s_ctl[0]) {
                 // (DETECT: as well -- to k_join's list-mode build)
                 if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             } else if constexpr (DETECT) {
@@ -2517,7 +2546,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                 // signature collision.
                 // (more suspects than sus[] holds: every live slot checks)
                 bool twin = false;
-                const unsigned nsus = s_nsus;
+                const unsigned nsus = s_ctl[3];
                 const bool all = nsus > kSusCap;
                 for (unsigned q = threadIdx.x; q < (all ? (unsigned)TS : nsus) && !twin; q += NT) {
                     unsigned slot, h;
@@ -2545,9 +2574,9 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                         h = (h + 1u) & kBMask;
                     }
                 }
-                if (twin) s_dup = 1u;
+                if (twin) s_ctl[1] = 1u;
                 __syncthreads();
-                if (threadIdx.x == 0 && s_dup && !dup_sent) {
+                if (threadIdx.x == 0 && s_ctl[1] && !dup_sent) {
                     __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     dup_sent = true;
                 }
@@ -2652,7 +2681,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                         const unsigned xm = wave_incl_add(cntm);
                         if (cntm) {
                             s_mpre[threadIdx.x] = xm - cntm;
-                            s_dup = 1u;
+                            s_ctl[1] = 1u;
                         }
                         if (lane == 63) s_cw[SI * NW + wv] = xm;
                     }
@@ -2690,7 +2719,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                             }
                             // a probe row met a repeated build key: the
                             // context's repeat flag, once per workgroup (k_join)
-                            if (s_dup && !dup_sent) {
+                            if (s_ctl[1] && !dup_sent) {
                                 __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                 dup_sent = true;
                             }
@@ -2720,6 +2749,10 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                 }
             }
             __syncthreads();   // table reused by the next item
+            if constexpr (DBL) {
+                bcnt = bcnt == sm.bcnt ? sm.bcnt2 : sm.bcnt;
+                s_ctl = s_ctl == sm.s_ctl ? sm.s_ctl2 : sm.s_ctl;
+            }
         }
         if (!more) break;
         w = wn;
@@ -3493,8 +3526,8 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     u64 chb = (u64)kJoinSub * subb;
     const u64 want = (u64)s_runs / (16ull * (wide ? pg : pgn));
     if (want > chb) chb = (want + subb - 1) / subb * subb;
-    // heavy-first item order: int64 rows (static item striding); i32 rows
-    // claim items dynamically and k_join_grp lost 0.2 ms on REF-A with it
+    // heavy-first item order for int64 rows (longest items claimed first);
+    // i32 rows keep partition order (k_join_grp lost 0.2 ms on REF-A with it)
     const bool heavy_first = kHeavyFirst && wide;
     chunk_map_one(s.rstart, r.rstart, P, (unsigned)chb, work_start, work_owner, ws, st, heavy_first);
     const unsigned items = (unsigned)((u64)s_runs / chb + (u64)P + 1);
@@ -3546,8 +3579,10 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             // (k_join_u served mode 2 before round 5 in a launch of its own;
             // both bodies in one kernel spilled 20 B at the 80-VGPR cap.)
             a.modes = kModeUnique | kModeSome;
+            if (HJ_WIDE_DYN) a.next_item = next_item;
             HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
+            a.next_item = nullptr;
         }
     } else {
         // i32 rows: k_join_b (keys and row ids apart in LDS: a bucket's 4

@@ -369,10 +369,10 @@ def distributed_join(hj, rkey, rpay, skey, spay, group=None, capacity=None, phas
         # folded: rows arrive first-pass partitioned (one local pass fewer)
         _dbg("route folded", rkey.numel(), skey.numel(), sub)
         nb = 1 << sub
-        send_r, cr = hj.route(rkey, rpay, world, sub)
+        send_r, cr = hj.route(rkey, rpay, world, sub, slot="r")
         xr = RoutedExchange(send_r, cr, nb, group, max_rows, self_p2p)
         ev("s_route")   # S's share of the route phase: its first partition pass happens here
-        send_s, cs = hj.route(skey, spay, world, sub)
+        send_s, cs = hj.route(skey, spay, world, sub, slot="s")
         xs = RoutedExchange(send_s, cs, nb, group, max_rows, self_p2p, parts=s_parts)
         ev("routed")
         recv_r = xr.wait()

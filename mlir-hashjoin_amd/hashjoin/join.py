@@ -17,6 +17,7 @@ reference's i32 keys with i32 row ids.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -52,8 +53,10 @@ class HashJoin:
             raise RuntimeError("hj_ctx_create failed: " + lib.hj_last_error().decode())
         self._count = torch.zeros(1, dtype=torch.int64, device=self.device)
         self.key_bits = None
+        self._routed = {}   # slot -> (rows, 2) int64 routed-tuple buffer (route(..., slot=))
 
     def close(self):
+        self._routed = {}
         if getattr(self, "_ctx", None):
             lib.hj_ctx_destroy(self._ctx)
             self._ctx = None
@@ -199,12 +202,23 @@ class HashJoin:
         check(lib.hj_route_plan(int(n_build_global), int(nranks), C.byref(b)), "hj_route_plan")
         return b.value
 
-    def route(self, key, pay, nranks, sub_bits, stream=None):
+    def route(self, key, pay, nranks, sub_bits, stream=None, slot=None):
         """(n, 2) tuples grouped by (owner, bin), and the (nranks << sub_bits)
-        part sizes (int64 device tensor)."""
+        part sizes (int64 device tensor).  slot (e.g. "r" / "s"): the tuples
+        go to a buffer this HashJoin keeps for that slot -- allocated once,
+        placement-probed (placed_rows) -- and stay valid until the slot's next
+        route; None: a fresh tensor."""
         _need_cuda(key, pay)
         n = key.shape[0]
-        out = torch.empty((n, 2), dtype=torch.int64, device=self.device)
+        if slot is None:
+            out = torch.empty((n, 2), dtype=torch.int64, device=self.device)
+        else:
+            buf = self._routed.get(slot)
+            if buf is None or buf.shape[0] < n:
+                self._routed.pop(slot, None)
+                buf = placed_rows(n, self.device)
+                self._routed[slot] = buf
+            out = buf[:n]
         counts = torch.empty(nranks << sub_bits, dtype=torch.int64, device=self.device)
         check(lib.hj_dev_route_i64(self._ctx, _ptr(key), _ptr(pay), n, nranks, sub_bits, _ptr(out), _ptr(counts),
                                    _stream(self.device, stream)), "hj_dev_route_i64")
@@ -407,6 +421,51 @@ def stream_copy(src, dst, shape="persistent", stream=None):
           "hj_dev_stream_copy")
 
 
+# Routed-tuple buffers (the EXACT routing pass's destination) are drawn like
+# the bucket sets' row buffers in libhj.so (hj_capi.cpp ensure_rows): a
+# buffer of >= 1 GiB is probed (hj_placement_check: the partition pass's write
+# pattern against a flat write) and redrawn while pattern/flat > 1.12, up to 12
+# draws with 3x its size free; rejects are held until the choice, then
+# released to the driver.  HJ_PLACEMENT_PROBE=0 turns it off.
+PLACE_MIN_BYTES = 1 << 30
+PLACE_GOOD = 1.12
+PLACE_DRAWS = 12
+_py_place = {"probes": 0, "rejected": 0, "last_kept_ratio": 0.0, "worst_kept_ratio": 0.0}
+
+
+def placed_rows(rows, device):
+    """A (rows, 2) int64 device tensor at a placement the partition passes'
+    write pattern runs fast in (see PLACE_*)."""
+    rows = max(int(rows), 1)
+    nbytes = rows * 16
+    if nbytes < PLACE_MIN_BYTES or os.environ.get("HJ_PLACEMENT_PROBE", "1") == "0":
+        return torch.empty((rows, 2), dtype=torch.int64, device=device)
+    held, best, best_r, draws = [], None, float("inf"), 0
+    for k in range(PLACE_DRAWS):
+        if k > 0 and torch.cuda.mem_get_info(device)[0] < 3 * nbytes:
+            break
+        t = torch.empty((rows, 2), dtype=torch.int64, device=device)
+        r = C.c_double(0.0)
+        check(lib.hj_placement_check(_ptr(t), nbytes, C.byref(r)), "hj_placement_check")
+        draws += 1
+        if r.value < best_r:
+            if best is not None:
+                held.append(best)
+            best, best_r = t, r.value
+        else:
+            held.append(t)
+        if best_r <= PLACE_GOOD:
+            break
+    _py_place["probes"] += draws
+    _py_place["rejected"] += len(held)
+    _py_place["last_kept_ratio"] = round(best_r, 3)
+    _py_place["worst_kept_ratio"] = max(_py_place["worst_kept_ratio"], round(best_r, 3))
+    if held:
+        del held
+        torch.cuda.empty_cache()   # the rejects go back to the driver, not to torch's cache
+    return best
+
+
 def placement_stats():
     """Row-buffer placement probe counts of this process (hj_placement_stats):
     draws probed / rejected and the pattern/flat write ratio of the last and
@@ -415,7 +474,7 @@ def placement_stats():
     last, worst = C.c_double(0.0), C.c_double(0.0)
     lib.hj_placement_stats(C.byref(pr), C.byref(rj), C.byref(last), C.byref(worst))
     return {"probes": pr.value, "rejected": rj.value, "last_kept_ratio": round(last.value, 3),
-            "worst_kept_ratio": round(worst.value, 3)}
+            "worst_kept_ratio": round(worst.value, 3), "routed_tuples": dict(_py_place)}
 
 
 def partition_of(key: int, nparts: int) -> int:
