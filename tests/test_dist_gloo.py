@@ -132,7 +132,7 @@ class _CpuJoin:
         h = keys.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
         return (h >> np.uint64(64 - bits)).astype(np.int64)
 
-    def route(self, key, pay, nranks, sub):
+    def route(self, key, pay, nranks, sub, slot=None):
         self.calls["partition"] += 1
         g = nranks.bit_length() - 1
         k, p = key.numpy(), pay.numpy()
