@@ -2308,9 +2308,8 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
     auto &s_skip = sm.s_skip;   // i32 rows: the item goes to k_join_grp (many pairs per probe row)
     auto &s_mpre = sm.s_mpre;   // a thread's multi pairs before it in its wave (kept out of registers)
     // a.next_item (DETECT walks w += grid): iteration k claims the item of
-    // iteration k + 2 into s_next after its first barrier (DBL: after the
-    // build barrier, the first one it has), and the top of iteration k + 1
-    // reads it (a workgroup's first two items are static: blockIdx.x,
+    // iteration k + 2 at its top and stores it into s_next after its build
+    // barrier, and the top of iteration k + 1 reads it (a workgroup's first two items are static: blockIdx.x,
     // blockIdx.x + grid).  int64 rows claim since round 5: the double-buffered
     // words took the clear barrier and 4 VGPRs off the kernel, and the claim
     // no longer spills (round 3: 20 B, C3 -6 %); C3 join 2.46 -> 2.30 ms, C4
@@ -2424,6 +2423,14 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
         }
         const unsigned wn = dyn ? __builtin_amdgcn_readfirstlane(s_next) : w + gridDim.x;
         const bool more = wn < total;
+        // the claim of the item after next, issued now and stored into s_next
+        // after the build barrier (every thread has read s_next by then): its
+        // return is waited for only there, once the build has covered its
+        // latency (stored right after the claim, wave 0 waited for it -- and,
+        // vector memory counts retiring in order, for the S rows just
+        // issued -- before it could start its share of the build)
+        unsigned claim = 0u;
+        if (dyn && threadIdx.x == 0) claim = atomicAdd(a.next_item, 1u);
         u64 ner[RI], nes[SI];
         unsigned nnvr = 0, nnvs = 0;
         ItemDesc nx = it;
@@ -2437,7 +2444,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
             if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
             if (dyn) {   // (every thread has read s_next above; the claim is read next iteration)
                 __syncthreads();
-                if (threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
+                if (threadIdx.x == 0) s_next = 2u * gridDim.x + claim;
                 __syncthreads();
             }
         } else {
@@ -2465,8 +2472,6 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
                 if (threadIdx.x == 0) *(uint4 *)s_ctl = z4;
                 __syncthreads();
             }
-            // (DBL: no barrier above -- the claim waits for the build barrier)
-            if (dyn && !DBL && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
             // ---- build: every row's rank add issued before any is used
             bool bad = false;
             for (u64 r0 = it.r_lo;;) {
@@ -2533,7 +2538,7 @@ __device__ __forceinline__ void join_b_body(JoinArgs a, JoinBSmem<WIDE, NT, SI, 
             }
             if (bad) s_ctl[0] = 1u;
             __syncthreads();
-            if (dyn && DBL && threadIdx.x == 0) s_next = 2u * gridDim.x + atomicAdd(a.next_item, 1u);
+            if (dyn && threadIdx.x == 0) s_next = 2u * gridDim.x + claim;
             if (s_ctl[0]) {
                 // (DETECT: as well -- to k_join's list-mode build)
                 if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = w;
