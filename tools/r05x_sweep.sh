@@ -17,8 +17,8 @@ for l in open('gpurun_out/$TAG/bench.jsonl'):
     d=json.loads(l); r=d['roofline']
     print(d['config']['workload'][:8], d['ms_per_step'], 'frac', r.get('frac'), {k:round(v,3) for k,v in d['phase_ms'].items() if v}, d.get('placement',{}).get('rejected'))
 "
-HJ_PLACEMENT_PROBE=0 timeout -k 10 200 python -u tools/xp_place.py 10 C1 > gpurun_out/$TAG/c1_place_off.jsonl 2>> gpurun_out/$TAG/bench.err || echo "c1 off failed"
-timeout -k 10 200 python -u tools/xp_place.py 10 C1 > gpurun_out/$TAG/c1_place_on.jsonl 2>> gpurun_out/$TAG/bench.err || echo "c1 on failed"
+
+
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$TAG/trace_dist -o run -- \
     python3 $R/bench.py --config C3 --force-dist --no-cpu-baseline --no-host-leg --steps 5 --warmup 2 > $R/gpurun_out/$TAG/trace_dist.log 2>&1 || echo "trace rc=$?"
