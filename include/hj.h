@@ -118,11 +118,11 @@ int hj_ctx_last_timing_ex(hj_ctx *ctx, float ms[8]);
  * build side's repeated keys, sampled at build time over up to 64 partitions
  * -- never of an earlier join's statistics: HJ_JOIN_KERNEL_BUCKETED
  * (k_join_b), _STREAM (k_join_u, probe-heavy shape), _GROUPED (k_join_grp
- * over every item: i32 rows, most build keys repeated), _GENERAL (k_join
- * over every item: int64 rows, most build keys repeated); 0 if the last
- * probe was no radix join.  Items those kernels defer (INT64_MIN build keys,
- * oversized partitions) run k_join afterwards.  (_LINEAR, k_join_u outside
- * the stream shape, is no longer chosen since round 5.)  Synchronises. */
+ * over every item: most build keys repeated; i32 and, since round 5, int64
+ * rows); 0 if the last probe was no radix join.  Items those kernels defer
+ * (INT64_MIN build keys, oversized partitions) run k_join afterwards.
+ * (_LINEAR, k_join_u outside the stream shape, and _GENERAL, k_join over
+ * every int64 item, are no longer chosen since round 5.)  Synchronises. */
 #define HJ_JOIN_KERNEL_BUCKETED 1
 #define HJ_JOIN_KERNEL_LINEAR 2
 #define HJ_JOIN_KERNEL_STREAM 3

@@ -2801,9 +2801,18 @@ __global__ __launch_bounds__(NT, WPS) void k_join_b(JoinArgs a) {
 // step (profiles/r02_refa_join_ablation.txt).  Items of more than 63 runs
 // (> TS - 64 build rows) go to a.defer (k_join's rounds take them).  LIST: the items of a.list
 // (k_join_u's deferrals) instead of all.
-template <bool WRITE, int NT, int RI, int SI, bool LIST>
+// WIDE (int64 key / int64 payload rows, round 5): the same grouping over
+// 2048 slots -- gkey holds the key (EMPTY = INT64_MIN: an item with that
+// build key goes to a.defer), gcnt the counts, grow the payloads -- at two
+// workgroups per CU (48 KiB of LDS each; at three the writing kernel spilled
+// at 80 VGPRs); REF-A's keys as int64 rows (REF-A64) took k_join's
+// linear-probing rounds 10.8 ms.
+template <bool WIDE, bool WRITE, int NT, int RI, int SI, bool LIST>
 __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
-    constexpr int TSL = 12, TS = 1 << TSL;
+    typedef Row<WIDE> R;
+    typedef typename R::T T;
+    typedef typename std::conditional<WIDE, u64, unsigned>::type PT;   // payload (wide) / row id
+    constexpr int TSL = WIDE ? 11 : 12, TS = 1 << TSL;
     constexpr unsigned kMask = TS - 1;
     constexpr int NW = NT / 64;
     constexpr unsigned rb = (unsigned)(NW * RI), subb = (unsigned)(NW * SI);
@@ -2813,20 +2822,22 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
     constexpr unsigned rmax = ((unsigned)TS >> kRunLog) - 1u;
     constexpr int PER = TS / NT;                         // table slots per thread in the scan
     static_assert(TS % NT == 0 && PER <= 16, "slots per thread");
-    constexpr u64 kE = ~0ull;
+    // narrow: key << 32 | count, EMPTY all ones; wide: the key, EMPTY INT64_MIN
+    constexpr u64 kE = WIDE ? (u64)kEmptyKey64 : ~0ull;
     __shared__ u64 gkey[TS];
     __shared__ unsigned gend[TS];
-    __shared__ unsigned grow[TS];
+    __shared__ unsigned gcnt[WIDE ? TS : 1];
+    __shared__ PT grow[TS];
     __shared__ u64 wsum[16];
     __shared__ u64 s_base;
-    __shared__ unsigned s_rep;
+    __shared__ unsigned s_rep, s_bad;
     const bool use_list = LIST && join_uses_list(a);
     const unsigned total = use_list ? *a.list_n : a.work_start[a.P];
     if (!join_runs(a)) return;
-    const u64 *rrows = (const u64 *)a.r;
-    const u64 *srows = (const u64 *)a.s;
-    unsigned *orr = (unsigned *)a.out_r;
-    unsigned *oss = (unsigned *)a.out_s;
+    const T *rrows = (const T *)a.r;
+    const T *srows = (const T *)a.s;
+    PT *orr = (PT *)a.out_r;
+    PT *oss = (PT *)a.out_s;
     const unsigned wv0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> kRunLog);
     const unsigned lane = threadIdx.x & 63u;
     bool dup_sent = false;
@@ -2837,7 +2848,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
             e[i] = li < hi ? sload(list + li) : 0ull;
         }
     };
-    auto rows_of = [&](const u64 *rows, const u64 *e, u64 *v, int n) {
+    auto rows_of = [&](const T *rows, const u64 *e, T *v, int n) {
         unsigned ok = 0;
 #pragma unroll
         for (int i = 0; i < n; ++i) {
@@ -2847,16 +2858,19 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
         }
         return ok;
     };
+    // a slot's key / count
+    auto key_is = [&](u64 e, u64 key) { return WIDE ? e == key : (e >> 32) == key; };
+    auto count_at = [&](unsigned h, u64 e) -> unsigned { return WIDE ? gcnt[h] : (unsigned)e; };
     // slot of `key` (claimed when absent); the walk ends: <= TS keys per item
-    auto slot_of = [&](unsigned key) -> unsigned {
-        unsigned h = (unsigned)(rhash((u64)key) >> a.tshift) & kMask;
+    auto slot_of = [&](u64 key) -> unsigned {
+        unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
         while (true) {
             u64 e = gkey[h];
             if (e == kE) {
-                e = atomicCAS(&gkey[h], kE, (u64)key << 32);
+                e = atomicCAS(&gkey[h], kE, WIDE ? key : key << 32);
                 if (e == kE) return h;
             }
-            if ((unsigned)(e >> 32) == key) return h;
+            if (key_is(e, key)) return h;
             h = (h + 1) & kMask;
         }
     };
@@ -2868,11 +2882,14 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
             continue;
         }
         for (int j = threadIdx.x; j < TS / 2; j += NT) ((ulonglong2 *)gkey)[j] = make_ulonglong2(kE, kE);
-        if (threadIdx.x == 0) s_rep = 0u;
+        if constexpr (WIDE)
+            for (int j = threadIdx.x; j < TS; j += NT) gcnt[j] = 0u;
+        if (threadIdx.x == 0) s_rep = s_bad = 0u;
         __syncthreads();
         // ---- count: every row claims / finds its key's slot and adds 1
         const bool one_round = it.r_hi - it.r_lo <= (u64)rb;   // uniform: rows stay in registers
-        u64 rv[RI], er[RI];
+        T rv[RI];
+        u64 er[RI];
         unsigned rok = 0, rh[RI];
         for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
             ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
@@ -2881,18 +2898,30 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
             for (int i = 0; i < RI; ++i) {
                 rh[i] = 0u;
                 if (!((rok >> i) & 1u)) continue;
-                rh[i] = slot_of((unsigned)(rv[i] >> 32));
-                atomicAdd(&gkey[rh[i]], 1ull);
+                if (WIDE && R::key(rv[i]) == kE) {   // the EMPTY key: k_join's null handling takes the item
+                    s_bad = 1u;
+                    rok &= ~(1u << i);
+                    continue;
+                }
+                rh[i] = slot_of(R::key(rv[i]));
+                if constexpr (WIDE) atomicAdd(&gcnt[rh[i]], 1u);
+                else atomicAdd(&gkey[rh[i]], 1ull);
             }
         }
         __syncthreads();
+        if (WIDE && s_bad) {   // uniform
+            if (threadIdx.x == 0) a.defer[atomicAdd(a.defer_n, 1u)] = wi;
+            __syncthreads();   // (tables reused by the next item)
+            continue;
+        }
         // ---- group starts: exclusive scan of the counts in slot order
         {
             unsigned c[PER], sum = 0, rep = 0;
 #pragma unroll
             for (int j = 0; j < PER; ++j) {
-                const u64 e = gkey[threadIdx.x * PER + j];
-                c[j] = e == kE ? 0u : (unsigned)e;
+                const unsigned h = threadIdx.x * PER + j;
+                const u64 e = gkey[h];
+                c[j] = e == kE ? 0u : count_at(h, e);
                 rep |= c[j] > 1u ? 1u : 0u;
                 sum += c[j];
             }
@@ -2910,7 +2939,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
             if (threadIdx.x == 0) __hip_atomic_store(a.dup_flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             dup_sent = true;
         }
-        // ---- placement: row ids into their key's group
+        // ---- placement: payloads (row ids) into their key's group
         for (u64 r0 = it.r_lo; r0 < it.r_hi; r0 += rb) {
             if (!one_round) {
                 ents(a.r_runs, r0, r0 + rb < it.r_hi ? r0 + rb : it.r_hi, er, RI);
@@ -2919,14 +2948,15 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
 #pragma unroll
             for (int i = 0; i < RI; ++i) {
                 if (!((rok >> i) & 1u)) continue;
-                const unsigned h = one_round ? rh[i] : slot_of((unsigned)(rv[i] >> 32));
-                grow[atomicAdd(&gend[h], 1u)] = (unsigned)rv[i];
+                const unsigned h = one_round ? rh[i] : slot_of(R::key(rv[i]));
+                grow[atomicAdd(&gend[h], 1u)] = (PT)R::pay(rv[i]);
             }
         }
         __syncthreads();
         // ---- probe, one sub-chunk of S rows at a time
         for (u64 sb = it.s_lo; sb < it.s_hi; sb += subb) {
-            u64 es[SI], sv[SI];
+            u64 es[SI];
+            T sv[SI];
             ents(a.s_runs, sb, sb + subb < it.s_hi ? sb + subb : it.s_hi, es, SI);
             const unsigned sok = rows_of(srows, es, sv, SI);
             unsigned cnt[SI], st[SI];
@@ -2935,15 +2965,17 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
             for (int i = 0; i < SI; ++i) {
                 cnt[i] = st[i] = 0u;
                 if (!((sok >> i) & 1u)) continue;
-                const unsigned key = (unsigned)(sv[i] >> 32);
-                unsigned h = (unsigned)(rhash((u64)key) >> a.tshift) & kMask;
+                const u64 key = R::key(sv[i]);
+                // (wide: an S key equal to EMPTY ends at the first empty slot:
+                // no build row holds it, items with one were deferred above)
+                unsigned h = (unsigned)(rhash(key) >> a.tshift) & kMask;
                 u64 e = gkey[h];
-                while (e != kE && (unsigned)(e >> 32) != key) {
+                while (e != kE && !key_is(e, key)) {
                     h = (h + 1) & kMask;
                     e = gkey[h];
                 }
                 if (e != kE) {
-                    cnt[i] = (unsigned)e;
+                    cnt[i] = count_at(h, e);
                     st[i] = gend[h] - cnt[i];
                 }
                 mine += cnt[i];
@@ -2970,7 +3002,10 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
                         const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)cnt[i], l);
                         if (!c) continue;   // uniform
                         const unsigned s0 = (unsigned)__builtin_amdgcn_readlane((int)st[i], l);
-                        const unsigned sp = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)sv[i], l);
+                        const u64 spay = R::pay(sv[i]);
+                        PT sp = (PT)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)spay, l);
+                        if constexpr (WIDE)
+                            sp |= (PT)((u64)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(spay >> 32), l) << 32);
                         // (plain stores: a group's run starts and ends inside
                         // lines, and non-temporal stores skip the L2 that
                         // assembles them with the neighbouring rows' pairs)
@@ -2991,7 +3026,7 @@ __global__ __launch_bounds__(NT, 4) void k_join_grp(JoinArgs a) {
                     for (unsigned j = 0; j < cnt[i]; ++j, ++q) {
                         if (q < (u64)a.cap) {
                             orr[q] = grow[st[i] + j];
-                            oss[q] = (unsigned)sv[i];
+                            oss[q] = (PT)R::pay(sv[i]);
                         }
                     }
                 }
@@ -3030,6 +3065,8 @@ constexpr int kFastNT = kFastNTc, kFastRI = kFastRIc, kFastSI = kFastSIc, kFastW
 constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 3, kStreamWPS = 8;
 // grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
 constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
+// int64 rows: 512 threads x 3 + 3 rows over 2048 slots, two workgroups per CU (at three, 80 VGPRs spilled)
+constexpr int kGrpWideRI = 3, kGrpWideSI = 3, kGrpWidePerCU = 2;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
 // i32 rows: k_join_b over 8192 slots (keys and row ids apart: 64 KiB), 768
 // threads x 4 build + 4 probe rows, 6 waves per SIMD, 2 workgroups per CU;
@@ -3543,7 +3580,7 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
     unsigned *next_item = defer2_n + 1 + radix_join_items(pl, s_runs);
     hipLaunchKernelGGL(k_item_desc, dim3(blocks_for(items, 256)), dim3(256), 0, st, (const unsigned *)work_start,
                        (const unsigned *)work_owner, (const u64 *)s.rstart, (const u64 *)r.rstart, P, (unsigned)chb,
-                       (ItemDesc *)desc, defer_n, wide ? nullptr : defer2_n, next_item,
+                       (ItemDesc *)desc, defer_n, defer2_n, next_item,
                        heavy_first ? (const u64 *)ws.pcur : nullptr, counter);
     JoinArgs a;
     a.r = r.rows;
@@ -3588,6 +3625,27 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
             HJ_WR((k_join_b<true, true, kFastNT, kFastRI, kFastSI, kFastWPS>),
                   (k_join_b<true, false, kFastNT, kFastRI, kFastSI, kFastWPS>), kFastNT);
             a.next_item = nullptr;
+            // k_join_grp (int64 rows, 2048 slots, two workgroups per CU):
+            // k_join_b's deferrals, or every item when most build keys
+            // repeat; what it defers (INT64_MIN build keys, > 31 runs) goes
+            // to k_join below
+            a.modes = kModesAll;
+            a.list = defer_n + 1;
+            a.list_n = defer_n;
+            a.all_if_mode2 = true;
+            a.defer = defer2_n + 1;
+            a.defer_n = defer2_n;
+            {
+                const unsigned g3 = items < (unsigned)(kGrpWidePerCU * cu_count()) ? items
+                                                                                   : (unsigned)(kGrpWidePerCU * cu_count());
+                if (count_only)
+                    hipLaunchKernelGGL((k_join_grp<true, false, kGrpNT, kGrpWideRI, kGrpWideSI, true>), dim3(g3),
+                                       dim3(kGrpNT), 0, st, a);
+                else
+                    hipLaunchKernelGGL((k_join_grp<true, true, kGrpNT, kGrpWideRI, kGrpWideSI, true>), dim3(g3),
+                                       dim3(kGrpNT), 0, st, a);
+            }
+            a.all_if_mode2 = false;
         }
     } else {
         // i32 rows: k_join_b (keys and row ids apart in LDS: a bucket's 4
@@ -3616,17 +3674,16 @@ hipError_t radix_join(bool wide, const RadixPlan &pl, const RadixWork &ws, const
         a.all_if_mode2 = true;
         a.defer = defer2_n + 1;
         a.defer_n = defer2_n;
-        HJ_WR((k_join_grp<true, kGrpNT, kGrpRI, kGrpSI, true>), (k_join_grp<false, kGrpNT, kGrpRI, kGrpSI, true>), kGrpNT);
+        HJ_WR((k_join_grp<false, true, kGrpNT, kGrpRI, kGrpSI, true>), (k_join_grp<false, false, kGrpNT, kGrpRI, kGrpSI, true>), kGrpNT);
         a.all_if_mode2 = false;
     }
     // what the kernels above deferred (INT64_MIN build keys, oversized
     // partitions, full tables): k_join over that list, a persistent grid that
-    // exits at once when it is empty -- and, for int64 rows outside the
-    // stream shape, every item when the sample says most build keys repeat
+    // exits at once when it is empty
     a.modes = kModesAll;
-    a.list = wide ? defer_n + 1 : defer2_n + 1;
-    a.list_n = wide ? defer_n : defer2_n;
-    a.all_if_mode2 = wide && !stream_shape;
+    a.list = wide && stream_shape ? defer_n + 1 : defer2_n + 1;
+    a.list_n = wide && stream_shape ? defer_n : defer2_n;
+    a.all_if_mode2 = false;
     if (wide) HJ_WR((k_join<true, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
                     (k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), 512);
     else HJ_WR((k_join<false, true, kTableLog, 512, 0, kJoinItems, 4, 0, true>),
@@ -3749,7 +3806,7 @@ int join_kernel_choice(bool wide, bool stream, unsigned long long rows, unsigned
     const int m = sample_mode(rows, repeats);
     if (wide) {
         if (stream) return HJ_JOIN_KERNEL_STREAM;
-        return m == 2 ? HJ_JOIN_KERNEL_GENERAL : HJ_JOIN_KERNEL_BUCKETED;
+        return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_BUCKETED;
     }
     return m == 2 ? HJ_JOIN_KERNEL_GROUPED : HJ_JOIN_KERNEL_BUCKETED;
 }

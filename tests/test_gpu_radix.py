@@ -341,7 +341,7 @@ def test_join_kernel_choice_is_deterministic(oracle):
         sk64 = sk64.copy()
         sk64[:5000] = dk[:5000]
         exp_d = oracle.chained_join_i64(dk, dp, sk64, sp64, H=200)
-        # i64, keys in [1, 2000] (~90 % of the build rows repeat): k_join over every item
+        # i64, keys in [1, 2000] (~90 % of the build rows repeat): the grouped join over every item
         hk, hp = oracle.gen_uniform_i64(10, 1, 1, 2000, 20000)
         hs, hsp = oracle.gen_uniform_i64(10, 2, 1, 2000, 6000)
         exp_h = oracle.chained_join_i64(hk, hp, hs, hsp, H=200)
@@ -371,7 +371,7 @@ def test_join_kernel_choice_is_deterministic(oracle):
                ("u", lambda: i64(dk, dp, sk64, sp64, exp_d)), ("b", lambda: i64(pk_r, pk_p, pk_s, pk_sp, exp_pk)),
                ("g", lambda: i64(hk, hp, hs, hsp, exp_h)), ("u32", lambda: i32(uk, us, exp_u)),
                ("g", lambda: i64(hk, hp, hs, hsp, exp_h))]
-        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_b", "u32": "k_join_b", "g": "k_join"}
+        want_k = {"grp": "k_join_grp", "b": "k_join_b", "u": "k_join_b", "u32": "k_join_b", "g": "k_join_grp"}
         for i, (what, fn) in enumerate(seq):
             assert fn() == want_k[what], f"join {i} ({what})"
     finally:
