@@ -688,6 +688,8 @@ int dbuf(hj_ctx *c, int i, size_t bytes, void **p) {
 // Copy a strided host memref (aligned + offset, size, stride) into device
 // buffer `dst` (contiguous).  shared.cpp reads through the aligned pointer
 // (shared.cpp:40, :67, :148); we additionally honour offset and stride.
+// (a plain pageable copy: a page-locked staging mirror of d2h below ran the
+// count's 537-MB upload slower, 20-21 -> 25-26 ms, profiles/r05/r05zi_*)
 template <class T>
 int upload(void *dst, const T *aligned, int64_t off, int64_t size, int64_t stride, hipStream_t st) {
     if (size <= 0) return HJ_OK;
@@ -1019,20 +1021,94 @@ HostRel rel64(const int64_t *k, int64_t k_off, int64_t k_stride, const int64_t *
     return HostRel{k, k_off, k_stride, p, p_off, p_stride, n};
 }
 
+// ---- device -> pageable host memory through page-locked staging.  A plain
+// hipMemcpy into a pageable buffer (the caller's memref) ran at ~17 GB/s
+// (bench host_memref: 2 x 134 MB in 16 ms); here 32-MiB chunks are DMA'd into
+// one of two page-locked buffers while the host copies the previous chunk out
+// with up to 8 threads (chunked).  The staging pairs are process-wide, taken
+// from a free list (concurrent host joins each take their own pair).
+constexpr size_t kStageChunk = size_t(32) << 20;
+constexpr size_t kStageMin = size_t(16) << 20;   // below this: one plain copy
+struct Staging {
+    void *p[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+std::mutex g_stage_mu;
+std::vector<Staging *> g_stage_free;
+
+Staging *stage_take() {
+    {
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        if (!g_stage_free.empty()) {
+            Staging *s = g_stage_free.back();
+            g_stage_free.pop_back();
+            return s;
+        }
+    }
+    Staging *s = new Staging;
+    bool ok = true;
+    for (int i = 0; i < 2 && ok; ++i) {
+        ok = hipHostMalloc(&s->p[i], kStageChunk, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev[i], hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        for (int i = 0; i < 2; ++i) {
+            if (s->p[i]) (void)hipHostFree(s->p[i]);
+            if (s->ev[i]) (void)hipEventDestroy(s->ev[i]);
+        }
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+void stage_give(Staging *s) {
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    g_stage_free.push_back(s);
+}
+
+int d2h(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    if (bytes == 0) return HJ_OK;
+    Staging *sg = bytes >= kStageMin ? stage_take() : nullptr;
+    if (!sg) {
+        HJ_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        HJ_HIP(hipStreamSynchronize(st));
+        return HJ_OK;
+    }
+    const size_t nch = (bytes + kStageChunk - 1) / kStageChunk;
+    auto len_of = [&](size_t i) { return i + 1 < nch ? kStageChunk : bytes - i * kStageChunk; };
+    auto issue = [&](size_t i) -> hipError_t {
+        hipError_t e = hipMemcpyAsync(sg->p[i & 1], (const char *)src + i * kStageChunk, len_of(i),
+                                      hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipEventRecord(sg->ev[i & 1], st);
+        return e;
+    };
+    hipError_t e = issue(0);
+    for (size_t i = 0; i < nch && e == hipSuccess; ++i) {
+        // chunk i + 1 lands in the buffer chunk i - 1 was copied out of
+        if (i + 1 < nch) e = issue(i + 1);
+        if (e == hipSuccess) e = hipEventSynchronize(sg->ev[i & 1]);
+        if (e != hipSuccess) break;
+        char *out = (char *)dst + i * kStageChunk;
+        const char *in = (const char *)sg->p[i & 1];
+        chunked((int64_t)len_of(i), 1, [&](int64_t a, int64_t b) { std::memcpy(out + a, in + a, (size_t)(b - a)); });
+    }
+    if (e != hipSuccess) (void)hipStreamSynchronize(st);   // (nothing left in flight into the staging)
+    stage_give(sg);
+    HJ_HIP(e);
+    return HJ_OK;
+}
+
 // Device column -> strided host memref.
 template <class T>
 int download(T *aligned, int64_t off, int64_t size, int64_t stride, const void *src, hipStream_t st) {
     if (size <= 0) return HJ_OK;
     if (!aligned) HJ_FAIL(HJ_ERR_ARG, "null output memref");
     T *base = aligned + off;
-    if (stride == 1) {
-        HJ_HIP(hipMemcpyAsync(base, src, sizeof(T) * (size_t)size, hipMemcpyDeviceToHost, st));
-        HJ_HIP(hipStreamSynchronize(st));
-        return HJ_OK;
-    }
+    if (stride == 1) return d2h(base, src, sizeof(T) * (size_t)size, st);
     std::vector<T> tmp((size_t)size);
-    HJ_HIP(hipMemcpyAsync(tmp.data(), src, sizeof(T) * (size_t)size, hipMemcpyDeviceToHost, st));
-    HJ_HIP(hipStreamSynchronize(st));
+    HJ_TRY(d2h(tmp.data(), src, sizeof(T) * (size_t)size, st));
     for (int64_t i = 0; i < size; ++i) base[i * stride] = tmp[(size_t)i];
     return HJ_OK;
 }
@@ -1045,9 +1121,8 @@ int fill_result(D *res, const void *d_r, const void *d_s, int64_t m, hipStream_t
     if (!buf) HJ_FAIL(HJ_ERR_NOMEM, "malloc result");
     if (m > 0) {
         std::vector<T> a((size_t)m), b((size_t)m);
-        HJ_HIP(hipMemcpyAsync(a.data(), d_r, sizeof(T) * (size_t)m, hipMemcpyDeviceToHost, st));
-        HJ_HIP(hipMemcpyAsync(b.data(), d_s, sizeof(T) * (size_t)m, hipMemcpyDeviceToHost, st));
-        HJ_HIP(hipStreamSynchronize(st));
+        HJ_TRY(d2h(a.data(), d_r, sizeof(T) * (size_t)m, st));
+        HJ_TRY(d2h(b.data(), d_s, sizeof(T) * (size_t)m, st));
         for (int64_t i = 0; i < m; ++i) {
             buf[2 * i] = a[(size_t)i];
             buf[2 * i + 1] = b[(size_t)i];
