@@ -493,3 +493,28 @@ def test_global_table_vs_oracle(oracle, case):
         assert oracle.same_multiset(o_r.cpu().numpy(), o_s.cpu().numpy(), *exp)
     finally:
         hj.close()
+
+
+def test_memref_outputs_through_staging():
+    """Outputs above the 16-MiB staging threshold (hj_capi.cpp d2h: 32-MiB
+    page-locked chunks, several in flight, copied out by host threads) land
+    intact in a contiguous and in a strided host memref: 2^22-row PK-FK
+    (32 MiB per output column), every S row once with its R match."""
+    n = 1 << 22
+    rk, rp, sk, sp = (t.cpu().numpy() for t in hashjoin.gen_pkfk(99, n, n))
+    m = MR.count_i64(rk, rp, sk, sp)
+    assert m == n
+    o_r = np.empty(m, np.int64)
+    o_s = np.empty(m, np.int64)
+    assert MR.probe_i64(rk, rp, sk, sp, o_r, o_s) == 0
+    # gen_pkfk payloads are row ids: key of each pair's R and S row agree,
+    # and every S row appears exactly once
+    assert np.array_equal(np.sort(o_s), np.arange(n, dtype=np.int64))
+    assert np.array_equal(rk[o_r], sk[o_s])
+    # strided outputs (every other element of a 2m buffer) through the same path
+    big_r = np.full(2 * m, -1, np.int64)
+    big_s = np.full(2 * m, -1, np.int64)
+    assert MR.probe_i64(rk, rp, sk, sp, big_r[::2], big_s[::2]) == 0
+    assert np.array_equal(np.sort(big_s[::2]), np.arange(n, dtype=np.int64))
+    assert np.array_equal(rk[big_r[::2]], sk[big_s[::2]])
+    assert (big_r[1::2] == -1).all() and (big_s[1::2] == -1).all()
