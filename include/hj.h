@@ -264,7 +264,7 @@ int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void 
 /* Placement of the radix bucket sets' row buffers (diagnostics, no reference
  * counterpart).  A row buffer of >= 1 GiB (buckets >= 8 KiB) is probed when allocated: the
  * partition pass's write pattern against a flat write of the same bytes
- * (some physical placements run the pattern 25-35 % slower), redrawn up to 12
+ * (some physical placements run the pattern 25-35 % slower), redrawn up to 24
  * times while slow, best draw kept; HJ_PLACEMENT_PROBE=0 in the environment
  * turns the probe off.  Process-wide counts since load: draws probed, draws
  * rejected, and the pattern/flat ratio of the last and of the worst kept

@@ -424,12 +424,12 @@ def stream_copy(src, dst, shape="persistent", stream=None):
 # Routed-tuple buffers (the EXACT routing pass's destination) are drawn like
 # the bucket sets' row buffers in libhj.so (hj_capi.cpp ensure_rows): a
 # buffer of >= 1 GiB is probed (hj_placement_check: the partition pass's write
-# pattern against a flat write) and redrawn while pattern/flat > 1.12, up to 12
+# pattern against a flat write) and redrawn while pattern/flat > 1.12, up to 24
 # draws with 3x its size free; rejects are held until the choice, then
 # released to the driver.  HJ_PLACEMENT_PROBE=0 turns it off.
 PLACE_MIN_BYTES = 1 << 30
 PLACE_GOOD = 1.12
-PLACE_DRAWS = 12
+PLACE_DRAWS = 24
 _py_place = {"probes": 0, "rejected": 0, "last_kept_ratio": 0.0, "worst_kept_ratio": 0.0}
 
 
