@@ -467,16 +467,15 @@ def main():
             cap = NS
         out_r = torch.empty(max(cap, 1), dtype=odt, device="cuda")
         out_s = torch.empty_like(out_r)
-        hj.set_timing(True)
+        # phase times from HIP events recorded inside every step, summed
+        # after the steps (hj_ctx_timing_accumulate): the steps run back to
+        # back with no host synchronisation between them; M (cnt) is read
+        # once the timed steps are over
+        hj.accumulate_timing(True)
 
         def step(acc):
             hj.build_table(rk, rp)
             hj.probe_relation(sk, sp, out_r, out_s, count=cnt)
-            t = hj.last_timing()          # synchronises: the step ends with M known on the host
-            if acc:
-                for k in ("init", "build", "probe", "probe_partition", "probe_join"):
-                    phases[k] += max(0.0, t[k])
-            last["m"] = int(cnt.item())
     else:
         # strong scaling over the GLOBAL relations; output stays distributed
         hj.allocate_hash_table(2 * nr, 64)
@@ -504,6 +503,8 @@ def main():
     for _ in range(a.warmup):
         step(False)
     torch.cuda.synchronize()
+    if not use_dist:
+        hj.timing_totals()   # (drops the warmup steps' times)
     if use_dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -513,6 +514,13 @@ def main():
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if not use_dist:
+        tot = hj.timing_totals()
+        if tot["steps"] != a.steps:
+            raise SystemExit(f"timing covered {tot['steps']} steps, expected {a.steps}")
+        for k in ("init", "build", "probe", "probe_partition", "probe_join"):
+            phases[k] += max(0.0, tot[k])
+        last["m"] = int(cnt.item())
 
     m_local = last["m"]
     per_rank = None

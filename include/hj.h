@@ -113,6 +113,16 @@ int hj_ctx_last_timing(hj_ctx *ctx, float ms[4]);
 /* Same plus the probe's split: [4] probe-side partitioning (RADIX, else 0),
  * [5] probe/join kernel; [6], [7] reserved (-1). */
 int hj_ctx_last_timing_ex(hj_ctx *ctx, float ms[8]);
+/* Accumulating timing (enable = 1; turns timing on): every build starts a
+ * new event set of a 64-set ring and a set is read back only when the ring
+ * comes round to it, so back-to-back build + probe steps run with no host
+ * synchronisation between them (a probe repeated without a build replaces
+ * that set's probe times).  Enabling again, or 0, drops what was recorded.
+ * hj_ctx_timing_totals sums every recorded set (synchronises on them) into
+ * ms[0..5] as hj_ctx_last_timing_ex orders them, *sets = how many, and
+ * starts the totals again; HJ_ERR_STATE unless accumulating. */
+int hj_ctx_timing_accumulate(hj_ctx *ctx, int enable);
+int hj_ctx_timing_totals(hj_ctx *ctx, float ms[8], long long *sets);
 /* RADIX: the join kernel of the last probe.  A pure function of the row
  * width, the probe / build size ratio (>= 8: the probe-heavy shape) and the
  * build side's repeated keys, sampled at build time over up to 64 partitions

@@ -141,12 +141,25 @@ struct hj_ctx {
     Buf rows_kx, rows_ky, rows_px, rows_py;   // row materialisation: key columns, pair row ids
     Buf sel_tiles, sel_sums;                  // selection: per-tile counts (then offsets), scan sums
     Buf route_hist, route_sums;               // folded routing: (bin, workgroup) slot bases, scan sums
-    // timing
+    // timing: the records go to event set `cur`.  Accumulating mode
+    // (hj_ctx_timing_accumulate) moves to the next set of a ring at every
+    // build and reads a set back only when the ring comes round to it again
+    // or the totals are asked for, so back-to-back build + probe steps need
+    // no host synchronisation between them.
+    static constexpr int kEvSets = 64;
+    struct EvSet {
+        hipEvent_t ev[kEvCount];
+        bool rec[4] = {false, false, false, false};
+        bool rec_mid = false;
+    };
     bool timing = false;
-    bool ev_ready = false;
-    hipEvent_t ev[kEvCount];
-    bool rec[4] = {false, false, false, false};
-    bool rec_mid = false;
+    bool ev_ready = false;   // set 0 created
+    bool acc = false;        // accumulating (every set created)
+    int cur = 0;
+    EvSet sets[kEvSets];
+    double tot[6] = {0, 0, 0, 0, 0, 0};
+    long long tot_sets = 0;
+    EvSet &evs() { return sets[cur]; }
     // host memref path.  One host thread at a time per context: every host
     // entry point holds host_mu (they share the staging buffers, dcount and
     // host_stream).
@@ -247,7 +260,53 @@ hj::TableDev table_dev(const hj_ctx *c) {
 }
 
 void record(hj_ctx *c, int ev, hipStream_t st) {
-    if (c->timing && c->ev_ready) (void)hipEventRecord(c->ev[ev], st);
+    if (c->timing && c->ev_ready) (void)hipEventRecord(c->evs().ev[ev], st);
+}
+
+// ms of one event set's phases: init, build, probe, routing partition,
+// probe-side partitioning, join (-1: not recorded)
+int set_ms(hj_ctx::EvSet &s, float ms[8]) {
+    for (int i = 0; i < 8; ++i) ms[i] = -1.0f;
+    auto el = [&](int a, int b, float *out) -> int {
+        HJ_HIP(hipEventSynchronize(s.ev[b]));
+        HJ_HIP(hipEventElapsedTime(out, s.ev[a], s.ev[b]));
+        return HJ_OK;
+    };
+    if (s.rec[0]) HJ_TRY(el(kEvInit0, kEvInit1, &ms[0]));
+    if (s.rec[1]) HJ_TRY(el(kEvInit1, kEvBuild1, &ms[1]));
+    if (s.rec[2]) HJ_TRY(el(kEvProbe0, kEvProbe1, &ms[2]));
+    if (s.rec[3]) HJ_TRY(el(kEvPart0, kEvPart1, &ms[3]));
+    if (s.rec[2]) {
+        if (s.rec_mid) {
+            HJ_TRY(el(kEvProbe0, kEvProbeMid, &ms[4]));
+            HJ_TRY(el(kEvProbeMid, kEvProbe1, &ms[5]));
+        } else {
+            ms[4] = 0.0f;
+            ms[5] = ms[2];
+        }
+    }
+    return HJ_OK;
+}
+
+// accumulating mode: add set k's phases to the totals and forget them
+int fold_set(hj_ctx *c, int k) {
+    hj_ctx::EvSet &s = c->sets[k];
+    if (!(s.rec[0] || s.rec[1] || s.rec[2] || s.rec[3])) return HJ_OK;
+    float ms[8];
+    HJ_TRY(set_ms(s, ms));
+    for (int i = 0; i < 6; ++i)
+        if (ms[i] > 0.0f) c->tot[i] += ms[i];
+    ++c->tot_sets;
+    s.rec[0] = s.rec[1] = s.rec[2] = s.rec[3] = s.rec_mid = false;
+    return HJ_OK;
+}
+
+// a build starts a step: accumulating, it records into the ring's next set
+// (summing what that set held first: a ring's length of steps ago)
+int timing_advance(hj_ctx *c) {
+    if (!c->acc || !c->timing) return HJ_OK;
+    c->cur = (c->cur + 1) % hj_ctx::kEvSets;
+    return fold_set(c, c->cur);
 }
 
 int ensure_buf(Buf &b, size_t bytes) {
@@ -445,6 +504,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     if (layout == kNarrow && src.n > 0x7fffffffll) HJ_FAIL(HJ_ERR_ARG, "i32 row ids: build side must have < 2^31 rows");
     HJ_TRY(set_device(c));
     HJ_TRY(ensure_meta(c, 64));
+    HJ_TRY(timing_advance(c));
     c->layout = layout;
     c->n_build = src.n;
     c->used = choose_strategy(c, src.n);
@@ -475,7 +535,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
         trace("build: R partitioned", st, (long long)c->plan.total_bits);
         if (!c->dual) {
             record(c, kEvBuild1, st);
-            c->rec[0] = c->rec[1] = c->timing;
+            c->evs().rec[0] = c->evs().rec[1] = c->timing;
             return HJ_OK;
         }
     }
@@ -487,7 +547,7 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     if (!c->dual) record(c, kEvInit1, st);
     HJ_HIP(hj::launch_build(t, layout, src, st));
     record(c, kEvBuild1, st);
-    c->rec[0] = c->rec[1] = c->timing;
+    c->evs().rec[0] = c->evs().rec[1] = c->timing;
     return HJ_OK;
 }
 
@@ -523,8 +583,8 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
         c->join_stream = stream;
         trace("probe: joined", st, cap);
         record(c, kEvProbe1, st);
-        c->rec[2] = c->timing;
-        c->rec_mid = c->timing;
+        c->evs().rec[2] = c->timing;
+        c->evs().rec_mid = c->timing;
         return HJ_OK;
     }
     HJ_HIP(hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
@@ -538,8 +598,8 @@ int do_probe(hj_ctx *c, int layout, const hj::SrcDev &src, void *out_r, void *ou
     HJ_TRY(ensure_buf(c->slow, slow_cap * sizeof(unsigned)));
     HJ_HIP(hj::launch_probe(table_dev(c), layout, src, out, count_only, (unsigned *)c->slow.p, slow_cap, st));
     record(c, kEvProbe1, st);
-    c->rec[2] = c->timing;
-    c->rec_mid = false;
+    c->evs().rec[2] = c->timing;
+    c->evs().rec_mid = false;
     return HJ_OK;
 }
 
@@ -553,7 +613,7 @@ int do_partition(hj_ctx *c, const hj::SrcDev &src, int nparts, int64_t *out, uin
     record(c, kEvPart0, st);
     HJ_HIP(hj::launch_partition(src, nparts, out, (unsigned long long *)d_counts, c->meta + 8, st));
     record(c, kEvPart1, st);
-    c->rec[3] = c->timing;
+    c->evs().rec[3] = c->timing;
     return HJ_OK;
 }
 
@@ -1276,8 +1336,8 @@ void hj_ctx_destroy(hj_ctx *c) {
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
                    &c->route_hist, &c->route_sums})
         free_buf(*b);
-    if (c->ev_ready)
-        for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->ev[i]);
+    for (int k = 0; k < (c->acc ? hj_ctx::kEvSets : c->ev_ready ? 1 : 0); ++k)
+        for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->sets[k].ev[i]);
     {
         std::lock_guard<std::mutex> lk(g_default_mu);
         for (auto it = g_default.begin(); it != g_default.end(); ++it)
@@ -1352,10 +1412,42 @@ int hj_ctx_set_timing(hj_ctx *c, int enable) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     HJ_TRY(set_device(c));
     if (enable && !c->ev_ready) {
-        for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->ev[i]));
+        for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->sets[0].ev[i]));
         c->ev_ready = true;
     }
     c->timing = enable != 0;
+    return HJ_OK;
+}
+
+int hj_ctx_timing_accumulate(hj_ctx *c, int enable) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    if (enable) HJ_TRY(hj_ctx_set_timing(c, 1));
+    if (enable && !c->acc) {
+        for (int k = 1; k < hj_ctx::kEvSets; ++k)
+            for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->sets[k].ev[i]));
+        c->acc = true;
+    }
+    if (!c->acc) return HJ_OK;
+    // a fresh start: nothing recorded so far counts
+    for (auto &s : c->sets) s.rec[0] = s.rec[1] = s.rec[2] = s.rec[3] = s.rec_mid = false;
+    for (double &t : c->tot) t = 0.0;
+    c->tot_sets = 0;
+    if (!enable) {
+        // (the sets stay created; set `cur` keeps taking the records)
+        c->acc = false;
+    }
+    return HJ_OK;
+}
+
+int hj_ctx_timing_totals(hj_ctx *c, float ms[8], long long *sets) {
+    if (!c || !ms || !sets) HJ_FAIL(HJ_ERR_ARG, "null argument");
+    if (!c->acc) HJ_FAIL(HJ_ERR_STATE, "timing totals need hj_ctx_timing_accumulate(c, 1)");
+    HJ_TRY(set_device(c));
+    for (int k = 1; k <= hj_ctx::kEvSets; ++k) HJ_TRY(fold_set(c, (c->cur + k) % hj_ctx::kEvSets));
+    for (int i = 0; i < 8; ++i) ms[i] = i < 6 ? (float)c->tot[i] : -1.0f;
+    *sets = c->tot_sets;
+    for (double &t : c->tot) t = 0.0;
+    c->tot_sets = 0;
     return HJ_OK;
 }
 
@@ -1364,25 +1456,7 @@ int hj_ctx_last_timing_ex(hj_ctx *c, float ms[8]) {
     for (int i = 0; i < 8; ++i) ms[i] = -1.0f;
     if (!c->ev_ready) return HJ_OK;
     HJ_TRY(set_device(c));
-    auto el = [&](int a, int b, float *out) -> int {
-        HJ_HIP(hipEventSynchronize(c->ev[b]));
-        HJ_HIP(hipEventElapsedTime(out, c->ev[a], c->ev[b]));
-        return HJ_OK;
-    };
-    if (c->rec[0]) HJ_TRY(el(kEvInit0, kEvInit1, &ms[0]));
-    if (c->rec[1]) HJ_TRY(el(kEvInit1, kEvBuild1, &ms[1]));
-    if (c->rec[2]) HJ_TRY(el(kEvProbe0, kEvProbe1, &ms[2]));
-    if (c->rec[3]) HJ_TRY(el(kEvPart0, kEvPart1, &ms[3]));
-    if (c->rec[2]) {
-        if (c->rec_mid) {
-            HJ_TRY(el(kEvProbe0, kEvProbeMid, &ms[4]));
-            HJ_TRY(el(kEvProbeMid, kEvProbe1, &ms[5]));
-        } else {
-            ms[4] = 0.0f;
-            ms[5] = ms[2];
-        }
-    }
-    return HJ_OK;
+    return set_ms(c->evs(), ms);
 }
 
 int hj_ctx_last_timing(hj_ctx *c, float ms[4]) {
@@ -1498,7 +1572,7 @@ int hj_dev_route_i64(hj_ctx *c, const int64_t *key, const int64_t *pay, int64_t 
     HJ_HIP(hj::radix_route(src_cols64(key, pay, n), rbits, out_tuples, (unsigned long long *)d_counts,
                            (unsigned long long *)c->route_hist.p, (unsigned long long *)c->route_sums.p, st));
     record(c, kEvPart1, st);
-    c->rec[3] = c->timing;
+    c->evs().rec[3] = c->timing;
     return HJ_OK;
 }
 
@@ -1512,6 +1586,7 @@ int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     hipStream_t st = (hipStream_t)stream;
     HJ_TRY(set_device(c));
     HJ_TRY(ensure_meta(c, 64));
+    HJ_TRY(timing_advance(c));
     // this rank's plan: the routing's bins are its first pass (skip = the
     // owner bits above them), one local pass of <= 9 bits below them
     hj::RadixPlan pl = hj::radix_plan(n, 0, true);
@@ -1545,7 +1620,7 @@ int hj_dev_build_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
                                       radix_work(c), bucket_set(c->rset), st));
     HJ_HIP(hj::radix_sample(true, pl, bucket_set(c->rset), c->meta + 2, st));
     record(c, kEvBuild1, st);
-    c->rec[0] = c->rec[1] = c->timing;
+    c->evs().rec[0] = c->evs().rec[1] = c->timing;
     return HJ_OK;
 }
 
@@ -1581,8 +1656,8 @@ int hj_dev_probe_routed_i64(hj_ctx *c, const int64_t *tuples, int64_t n, const u
     c->join_wide = true;
     c->join_stream = stream_shape;
     record(c, kEvProbe1, st);
-    c->rec[2] = c->timing;
-    c->rec_mid = c->timing;
+    c->evs().rec[2] = c->timing;
+    c->evs().rec_mid = c->timing;
     return HJ_OK;
 }
 

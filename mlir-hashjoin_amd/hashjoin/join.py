@@ -129,6 +129,22 @@ class HashJoin:
         check(lib.hj_ctx_last_timing_ex(self._ctx, a), "hj_ctx_last_timing_ex")
         return dict(zip(("init", "build", "probe", "partition", "probe_partition", "probe_join"), list(a)[:6]))
 
+    def accumulate_timing(self, enable=True):
+        """Per-step phase times with no host synchronisation between steps:
+        each build starts a new event set (hj_ctx_timing_accumulate);
+        timing_totals() sums them.  Enabling again drops what was recorded."""
+        check(lib.hj_ctx_timing_accumulate(self._ctx, 1 if enable else 0), "hj_ctx_timing_accumulate")
+
+    def timing_totals(self):
+        """Summed ms of every build + probe step since accumulate_timing() or
+        the last call (synchronises), with "steps": how many."""
+        a = (C.c_float * 8)()
+        n = C.c_longlong(0)
+        check(lib.hj_ctx_timing_totals(self._ctx, a, C.byref(n)), "hj_ctx_timing_totals")
+        d = dict(zip(("init", "build", "probe", "partition", "probe_partition", "probe_join"), list(a)[:6]))
+        d["steps"] = n.value
+        return d
+
     # -------------------------------------------------------------- phases
     def build_table(self, rkey, rpay=None, row_base=0, stream=None):
         """@initializeHashTable + @buildTable (join_v2.mlir:54-108)."""
