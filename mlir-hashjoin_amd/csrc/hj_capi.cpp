@@ -154,7 +154,8 @@ struct hj_ctx {
     };
     bool timing = false;
     bool ev_ready = false;   // set 0 created
-    bool acc = false;        // accumulating (every set created)
+    int ev_made = 0;         // sets created (1, or all of them once accumulating was asked for)
+    bool acc = false;        // accumulating
     int cur = 0;
     EvSet sets[kEvSets];
     double tot[6] = {0, 0, 0, 0, 0, 0};
@@ -1181,8 +1182,12 @@ int fill_result(D *res, const void *d_r, const void *d_s, int64_t m, hipStream_t
     if (!buf) HJ_FAIL(HJ_ERR_NOMEM, "malloc result");
     if (m > 0) {
         std::vector<T> a((size_t)m), b((size_t)m);
-        HJ_TRY(d2h(a.data(), d_r, sizeof(T) * (size_t)m, st));
-        HJ_TRY(d2h(b.data(), d_s, sizeof(T) * (size_t)m, st));
+        int rc = d2h(a.data(), d_r, sizeof(T) * (size_t)m, st);
+        if (rc == HJ_OK) rc = d2h(b.data(), d_s, sizeof(T) * (size_t)m, st);
+        if (rc != HJ_OK) {
+            std::free(buf);   // (the descriptor stays empty: allocated == NULL)
+            return rc;
+        }
         for (int64_t i = 0; i < m; ++i) {
             buf[2 * i] = a[(size_t)i];
             buf[2 * i + 1] = b[(size_t)i];
@@ -1336,7 +1341,7 @@ void hj_ctx_destroy(hj_ctx *c) {
                    &c->slow, &c->rows_kx, &c->rows_ky, &c->rows_px, &c->rows_py, &c->sel_tiles, &c->sel_sums,
                    &c->route_hist, &c->route_sums})
         free_buf(*b);
-    for (int k = 0; k < (c->acc ? hj_ctx::kEvSets : c->ev_ready ? 1 : 0); ++k)
+    for (int k = 0; k < c->ev_made; ++k)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->sets[k].ev[i]);
     {
         std::lock_guard<std::mutex> lk(g_default_mu);
@@ -1414,6 +1419,7 @@ int hj_ctx_set_timing(hj_ctx *c, int enable) {
     if (enable && !c->ev_ready) {
         for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->sets[0].ev[i]));
         c->ev_ready = true;
+        c->ev_made = 1;
     }
     c->timing = enable != 0;
     return HJ_OK;
@@ -1422,11 +1428,13 @@ int hj_ctx_set_timing(hj_ctx *c, int enable) {
 int hj_ctx_timing_accumulate(hj_ctx *c, int enable) {
     if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
     if (enable) HJ_TRY(hj_ctx_set_timing(c, 1));
-    if (enable && !c->acc) {
-        for (int k = 1; k < hj_ctx::kEvSets; ++k)
+    if (enable && c->ev_made < hj_ctx::kEvSets) {
+        for (int k = c->ev_made; k < hj_ctx::kEvSets; ++k) {
             for (int i = 0; i < kEvCount; ++i) HJ_HIP(hipEventCreate(&c->sets[k].ev[i]));
-        c->acc = true;
+            c->ev_made = k + 1;
+        }
     }
+    if (enable) c->acc = true;
     if (!c->acc) return HJ_OK;
     // a fresh start: nothing recorded so far counts
     for (auto &s : c->sets) s.rec[0] = s.rec[1] = s.rec[2] = s.rec[3] = s.rec_mid = false;
