@@ -3063,8 +3063,11 @@ constexpr int kFastNT = kFastNTc, kFastRI = kFastRIc, kFastSI = kFastSIc, kFastW
 // without it C2's join 6.49 -> 6.16 ms on one box (768 x 3+4: 6.25, 768 x
 // 2+5: 6.30, 1024 x 1+4: 6.47; profiles/r03_narrow_shapes.txt 8)
 constexpr int kStreamNT = 1024, kStreamRI = 2, kStreamSI = 3, kStreamWPS = 8;
-// grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS)
-constexpr int kGrpNT = 512, kGrpRI = 4, kGrpSI = 4;
+// grouped join (narrow rows with repeated keys): 512 threads, 2 workgroups per CU (64 KiB of LDS),
+// 3 build + 8 probe rows per thread (round 5; 4 + 4 before): a REF-A item's
+// probe rows in one sub-chunk, REF-A join 1.85 -> 1.79 ms (profiles/r05/r05zu_grouped_rows_ab.jsonl;
+// 4 + 8 1.80, 4 + 10 1.80, 3 + 5 / 4 + 5 unchanged; 110 VGPRs of the 128 two workgroups allow)
+constexpr int kGrpNT = 512, kGrpRI = 3, kGrpSI = 8;
 // int64 rows: 512 threads x 3 + 3 rows over 2048 slots, two workgroups per CU (at three, 80 VGPRs spilled)
 constexpr int kGrpWideRI = 3, kGrpWideSI = 3, kGrpWidePerCU = 2;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
