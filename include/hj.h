@@ -280,6 +280,16 @@ int hj_dev_stream_copy(const void *in, void *out, int64_t rows, int shape, void 
  * rejected, and the pattern/flat ratio of the last and of the worst kept
  * buffer (0 when none was probed).  Any pointer may be null. */
 void hj_placement_stats(long long *probes, long long *rejected, double *last_kept, double *worst_kept);
+/* Since round 6 a probe holds at most 2 rejected draws at once (a further
+ * reject frees the oldest) and draws again only while free memory is >= 3x
+ * the buffer.  out[0] draws probed, [1] rejected, [2] buffers that kept a
+ * slow draw (gave up), [3] of those, gave up because free memory ran short,
+ * [4] most rejected draws held at once; ratios as hj_placement_stats. */
+void hj_placement_stats_ex(long long out[5], double *last_kept, double *worst_kept);
+/* The pattern/flat ratio a draw must reach to be kept at once (default
+ * 1.12); returns the previous value, ratio <= 0 only reads it.  A knob for
+ * tests (a low ratio makes every draw a reject). */
+double hj_placement_set_good(double ratio);
 /* The same probe on a caller's device buffer of >= 4 MiB per CU (its
  * contents are overwritten): *ratio = pass-pattern time / flat-write time
  * (~1.0 good placement, 1.25-1.35 slow).  Synchronous on the default stream.

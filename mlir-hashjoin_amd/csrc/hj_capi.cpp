@@ -335,18 +335,25 @@ void free_buf(Buf &b) {
 // profiles/r05/r05t_place_micro.txt; the same pass into two such buffers: 1.46
 // vs 1.76 ms).  A large row buffer is therefore probed when it is allocated
 // (hj::placement_probe: the pass's pattern against a flat write, ~2 ms) and
-// redrawn while it is slow: up to kPlaceDraws allocations, the rejected ones
-// held until the choice is made (so the allocator cannot hand them back) and
-// then freed; the best draw is kept.  HJ_PLACEMENT_PROBE=0 turns it off.
+// redrawn while it is slow: up to kPlaceDraws allocations.  Rejected draws
+// are held (so the allocator cannot hand the same memory back), at most
+// kPlaceHeld of them at once -- a further reject frees the oldest held one --
+// and another draw is taken only while free memory is at least kPlaceSpare
+// times the buffer (the same rule as hashjoin.join.placed_rows); the best draw
+// is kept and the rest freed.  A buffer whose draws stopped before a good one
+// is a give-up, counted (and why) in hj_placement_stats_ex and in every bench
+// line.  HJ_PLACEMENT_PROBE=0 turns it off.
 // (smaller buffers, and 4-KiB buckets (i32 rows' final sets), probe too short
 // a pattern to judge: REF-B's sets were rejected 9 draws in 10 at unchanged
 // pass times, profiles/r05/r05y_*)
 constexpr size_t kPlaceMinBytes = size_t(1) << 30;
 constexpr size_t kPlaceMinBucket = size_t(8) << 10;
 constexpr int kPlaceDraws = 24;   // (a box where 86 % of draws were slow: r05_final)
-constexpr float kPlaceGood = 1.12f;                  // pattern / flat at a good placement: 0.98-1.05
+constexpr int kPlaceHeld = 2;     // rejected draws held at once
+constexpr size_t kPlaceSpare = 3; // another draw while free memory >= 3 x the buffer
+std::atomic<float> g_place_good{1.12f};   // pattern / flat at a good placement: 0.98-1.05
 struct PlaceStats {
-    long long probes = 0, rejected = 0;
+    long long probes = 0, rejected = 0, gave_up = 0, gave_up_low_mem = 0, held_max = 0;
     double worst_kept = 0.0, last_kept = 0.0;
 };
 PlaceStats g_place;
@@ -368,19 +375,26 @@ int ensure_rows(Buf &b, size_t bytes, size_t bucket_bytes) {
     int dev = 0, cus = 0;
     HJ_HIP(hipGetDevice(&dev));
     HJ_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    std::vector<Buf> rejected;
+    const float good = g_place_good.load();
+    std::vector<Buf> held;   // rejected draws still held (oldest first)
     Buf best;
     float best_r = 1e30f;
     int draws = 0;
+    long long rejected = 0, held_max = 0;
+    bool low_mem = false;
     for (; draws < kPlaceDraws; ++draws) {
         if (draws > 0) {
-            // another draw only with room for it and three times its size to spare
             size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < 4 * bytes) break;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < kPlaceSpare * bytes) {
+                (void)hipGetLastError();
+                low_mem = true;
+                break;
+            }
         }
         Buf cand;
         if (hipMalloc(&cand.p, bytes) != hipSuccess) {
             (void)hipGetLastError();
+            low_mem = true;
             break;
         }
         cand.bytes = bytes;
@@ -389,31 +403,48 @@ int ensure_rows(Buf &b, size_t bytes, size_t bucket_bytes) {
             (void)hipGetLastError();
             r = 0.0f;   // no verdict: take it
         }
+        Buf rej;
         if (r < best_r) {
-            if (best.p) rejected.push_back(best);
+            rej = best;
             best = cand;
             best_r = r;
         } else {
-            rejected.push_back(cand);
+            rej = cand;
         }
-        if (best_r <= kPlaceGood) {
+        if (rej.p) {
+            ++rejected;
+            held.push_back(rej);
+            if ((int)held.size() > kPlaceHeld) {
+                free_buf(held.front());
+                held.erase(held.begin());
+            }
+            if ((long long)held.size() > held_max) held_max = (long long)held.size();
+        }
+        if (best_r <= good) {
             ++draws;
             break;
         }
     }
-    for (Buf &x : rejected) free_buf(x);
+    for (Buf &x : held) free_buf(x);
     if (!best.p) HJ_FAIL(HJ_ERR_NOMEM, "hipMalloc radix rows " + std::to_string(bytes));
     b = best;
+    const bool gave_up = best_r > good;
     {
         std::lock_guard<std::mutex> lk(g_place_mu);
         g_place.probes += draws;
-        g_place.rejected += (long long)rejected.size();
+        g_place.rejected += rejected;
+        if (gave_up) {
+            ++g_place.gave_up;
+            if (low_mem) ++g_place.gave_up_low_mem;
+        }
+        if (held_max > g_place.held_max) g_place.held_max = held_max;
         g_place.last_kept = best_r;
         if (best_r > g_place.worst_kept) g_place.worst_kept = best_r;
     }
-    if (trace_on())
-        std::fprintf(stderr, "hj trace: rows placement %zu B: %d draw(s), kept pattern/flat %.3f\n", bytes, draws,
-                     (double)best_r);
+    if (trace_on() || (gave_up && low_mem))
+        std::fprintf(stderr, "hj %s: rows placement %zu B: %d draw(s), kept pattern/flat %.3f%s\n",
+                     trace_on() ? "trace" : "note", bytes, draws, (double)best_r,
+                     gave_up ? (low_mem ? " (gave up: free memory below 3x the buffer)" : " (gave up: draws spent)") : "");
     return HJ_OK;
 }
 
@@ -990,6 +1021,10 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
     const int esz = layout == kWide ? 8 : 4;
     hj_ctx::Memo &mm = c->memo;
     const int reuse = g_reuse.load();
+    // a memo an EXACT count left on this context after the mode moved on:
+    // its input copies (GBs at 2^28 rows) go now (hj_host_set_reuse frees
+    // those of the default contexts at once; user contexts' here)
+    if (mm.reuse == HJ_REUSE_EXACT && reuse != HJ_REUSE_EXACT && (!mm.cr.empty() || !mm.cs.empty())) mm.invalidate();
     Digest dr, ds;
     bool same_r = false, same_s = false;   // HJ_REUSE_EXACT: byte-equal to the count's inputs
     if (delivered) *delivered = false;
@@ -1087,26 +1122,37 @@ HostRel rel64(const int64_t *k, int64_t k_off, int64_t k_stride, const int64_t *
 // (bench host_memref: 2 x 134 MB in 16 ms); here 32-MiB chunks are DMA'd into
 // one of two page-locked buffers while the host copies the previous chunk out
 // with up to 8 threads (chunked).  The staging pairs are process-wide, taken
-// from a free list (concurrent host joins each take their own pair).
+// from a free list (concurrent host joins each take their own pair); a pair's
+// events belong to the device that was current when it was made, so a pair
+// is only handed out again on that device (an event recorded on
+// another device's stream is an invalid handle).
 constexpr size_t kStageChunk = size_t(32) << 20;
 constexpr size_t kStageMin = size_t(16) << 20;   // below this: one plain copy
 struct Staging {
     void *p[2] = {nullptr, nullptr};
     hipEvent_t ev[2] = {nullptr, nullptr};
+    int dev = -1;
 };
 std::mutex g_stage_mu;
 std::vector<Staging *> g_stage_free;
 
 Staging *stage_take() {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     {
         std::lock_guard<std::mutex> lk(g_stage_mu);
-        if (!g_stage_free.empty()) {
-            Staging *s = g_stage_free.back();
-            g_stage_free.pop_back();
+        for (size_t i = 0; i < g_stage_free.size(); ++i) {
+            if (g_stage_free[i]->dev != dev) continue;
+            Staging *s = g_stage_free[i];
+            g_stage_free.erase(g_stage_free.begin() + (std::ptrdiff_t)i);
             return s;
         }
     }
     Staging *s = new Staging;
+    s->dev = dev;
     bool ok = true;
     for (int i = 0; i < 2 && ok; ++i) {
         ok = hipHostMalloc(&s->p[i], kStageChunk, hipHostMallocDefault) == hipSuccess &&
@@ -1284,14 +1330,14 @@ int hj_host_set_reuse(int mode) {
     const int prev = g_reuse.exchange(mode);
     if (prev == HJ_REUSE_EXACT && mode != HJ_REUSE_EXACT) {
         // the EXACT copies can no longer be used: give their memory back
-        std::vector<hj_ctx *> ctxs;
-        {
-            std::lock_guard<std::mutex> lk(g_default_mu);
-            for (auto &kv : g_default) ctxs.push_back(kv.second);
-        }
-        for (hj_ctx *c : ctxs) {
-            std::lock_guard<std::mutex> host_lk(c->host_mu);
-            c->memo.invalidate();
+        // (the default contexts' now -- g_default_mu held throughout, so
+        // hj_ctx_destroy, which takes a context out of g_default before it
+        // frees anything, cannot free one under us; user contexts drop
+        // theirs at their next host join)
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        for (auto &kv : g_default) {
+            std::lock_guard<std::mutex> host_lk(kv.second->host_mu);
+            kv.second->memo.invalidate();
         }
     }
     return prev;
@@ -1326,6 +1372,14 @@ hj_ctx *hj_ctx_create(int device) {
 
 void hj_ctx_destroy(hj_ctx *c) {
     if (!c) return;
+    {   // out of the default registry first (hj_host_set_reuse walks it)
+        std::lock_guard<std::mutex> lk(g_default_mu);
+        for (auto it = g_default.begin(); it != g_default.end(); ++it)
+            if (it->second == c) {
+                g_default.erase(it);
+                break;
+            }
+    }
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     if (c->table) (void)hipFree(c->table);
@@ -1343,14 +1397,6 @@ void hj_ctx_destroy(hj_ctx *c) {
         free_buf(*b);
     for (int k = 0; k < c->ev_made; ++k)
         for (int i = 0; i < kEvCount; ++i) (void)hipEventDestroy(c->sets[k].ev[i]);
-    {
-        std::lock_guard<std::mutex> lk(g_default_mu);
-        for (auto it = g_default.begin(); it != g_default.end(); ++it)
-            if (it->second == c) {
-                g_default.erase(it);
-                break;
-            }
-    }
     delete c;
 }
 
@@ -2018,6 +2064,25 @@ void hj_placement_stats(long long *probes, long long *rejected, double *last_kep
     if (rejected) *rejected = g_place.rejected;
     if (last_kept) *last_kept = g_place.last_kept;
     if (worst_kept) *worst_kept = g_place.worst_kept;
+}
+
+void hj_placement_stats_ex(long long out[5], double *last_kept, double *worst_kept) {
+    std::lock_guard<std::mutex> lk(g_place_mu);
+    if (out) {
+        out[0] = g_place.probes;
+        out[1] = g_place.rejected;
+        out[2] = g_place.gave_up;
+        out[3] = g_place.gave_up_low_mem;
+        out[4] = g_place.held_max;
+    }
+    if (last_kept) *last_kept = g_place.last_kept;
+    if (worst_kept) *worst_kept = g_place.worst_kept;
+}
+
+double hj_placement_set_good(double ratio) {
+    const float prev = g_place_good.load();
+    if (ratio > 0.0) g_place_good.store((float)ratio);
+    return (double)prev;
 }
 
 int hj_placement_check(const void *buf, int64_t bytes, double *ratio) {

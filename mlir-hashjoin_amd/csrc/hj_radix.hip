@@ -1261,6 +1261,8 @@ struct JoinArgs {
     // before it left to it (k_join for int64 rows, k_join_grp for i32 rows),
     // so that launch and the mode-2 one are one launch (no exit-only launch)
     bool all_if_mode2 = false;
+    // k_join: exit at once when *skip_if_set != 0 (radix_detect's self-join)
+    const u64 *skip_if_set = nullptr;
 };
 
 constexpr unsigned kModeUnique = 1u, kModeSome = 2u, kModeMostlyRepeated = 4u;
@@ -1401,6 +1403,13 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     constexpr unsigned subb = (unsigned)SUBR >> kRunLog;     // runs per sub-chunk
     constexpr unsigned chb = (unsigned)kJoinSub * subb;      // runs per work item
     static_assert((rb << kRunLog) == RCAP && (subb << kRunLog) == SUBR, "rounds must be whole runs");
+    // A round loads RI rows per thread (runs lo + i * NW + wave) but steps
+    // the run cursor by rb: rows past RI * NT in a round would never be
+    // built.  Round 5's dropped int64 shape (512 threads over 2048 slots:
+    // RCAP 1280, RI 2 -> 1024 rows loaded per 1280 stepped) lost one build
+    // row in five in every deferred partition -- 16,986 of 20,942 pairs on a
+    // 1-bit plan.
+    static_assert(RI * NT == RCAP, "a build round must load exactly RCAP rows");
     // wide: EMPTY key INT64_MIN (rows with that key take the null path);
     // narrow: the all-ones word (row ids < 2^31 never produce it)
     constexpr u64 kEmpty = WIDE ? kEmptyKey64 : ~0ull;
@@ -1416,6 +1425,10 @@ __global__ __launch_bounds__(NT, WPS) void k_join(JoinArgs a) {
     const unsigned total = use_list ? *a.list_n : a.work_start[a.P];
     unsigned w = blockIdx.x;
     if (w >= total) return;
+    // (radix_detect's self-join of the deferred partitions: nothing to
+    // answer once a repeat is known -- and a hot key's copies would walk
+    // each other's chains, ~m^2 steps)
+    if (a.skip_if_set && __hip_atomic_load(a.skip_if_set, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const T *rrows = (const T *)a.r;
     const T *srows = (const T *)a.s;
     PT *orr = (PT *)a.out_r;
@@ -3788,6 +3801,11 @@ hipError_t radix_detect(bool wide, const RadixPlan &pl, const RadixWork &ws, con
     if (e != hipSuccess) return e;
     a.empty_s = false;
     a.counter = ws.pcur;
+    // (skipped when the launches above already found a repeat: a key that
+    // repeats m times inside one partition has >= 2 copies in some build
+    // round once m exceeds the rounds, so the self-join only ever runs over
+    // partitions whose keys repeat at most once per round)
+    a.skip_if_set = dup_flag;
     if (wide)
         hipLaunchKernelGGL((k_join<true, false, kTableLog, 512, 0, kJoinItems, 4, 0, true>), dim3(2 * cu_count()),
                            dim3(512), 0, st, a);

@@ -102,6 +102,8 @@ def _load():
         "hj_dev_select_i64": (_int, [_vp, _vp, _i64, _int, _i64, _vp, _vp, _i64, _vp, _vp]),
         "hj_dev_stream_copy": (_int, [_vp, _vp, _i64, _int, _vp]),
         "hj_placement_stats": (None, [_vp, _vp, _vp, _vp]),
+        "hj_placement_stats_ex": (None, [_vp, _vp, _vp]),
+        "hj_placement_set_good": (C.c_double, [C.c_double]),
         "hj_placement_check": (_int, [_vp, _i64, _vp]),
         "hj_select_f32": (_i64, [_vp, _vp, _i64, _i64, _i64, C.c_float, _vp, _vp, _i64, _i64, _i64]),
         "_mlir_ciface_hj_join_i32": (None, [_vp, _vp, _vp]),

@@ -440,57 +440,85 @@ def stream_copy(src, dst, shape="persistent", stream=None):
 # Routed-tuple buffers (the EXACT routing pass's destination) are drawn like
 # the bucket sets' row buffers in libhj.so (hj_capi.cpp ensure_rows): a
 # buffer of >= 1 GiB is probed (hj_placement_check: the partition pass's write
-# pattern against a flat write) and redrawn while pattern/flat > 1.12, up to 24
-# draws with 3x its size free; rejects are held until the choice, then
-# released to the driver.  HJ_PLACEMENT_PROBE=0 turns it off.
+# pattern against a flat write) and redrawn while pattern/flat > 1.12 (the
+# library's hj_placement_set_good value), up to 24 draws while free memory is
+# >= 3x the buffer, holding at most 2 rejected draws at once (a further reject
+# releases the oldest); the best draw is kept.  A buffer that keeps a slow
+# draw is a give-up, counted in placement_stats().  HJ_PLACEMENT_PROBE=0
+# turns it off.
 PLACE_MIN_BYTES = 1 << 30
-PLACE_GOOD = 1.12
 PLACE_DRAWS = 24
-_py_place = {"probes": 0, "rejected": 0, "last_kept_ratio": 0.0, "worst_kept_ratio": 0.0}
+PLACE_HELD = 2
+PLACE_SPARE = 3
+_py_place = {"probes": 0, "rejected": 0, "gave_up": 0, "gave_up_low_mem": 0, "held_max": 0,
+             "last_kept_ratio": 0.0, "worst_kept_ratio": 0.0}
 
 
 def placed_rows(rows, device):
     """A (rows, 2) int64 device tensor at a placement the partition passes'
-    write pattern runs fast in (see PLACE_*)."""
+    write pattern runs fast in (see PLACE_*).
+
+    The probe writes the candidate on the device's default HIP stream, so the
+    caller's streams are drained first (a block torch hands out may still be
+    in use by work queued on another stream).  Rejected draws are released to
+    the driver with torch.cuda.empty_cache(), which also releases every other
+    unused block torch has cached in this process (outside every timed
+    region; the allocation is once per exchange buffer)."""
     rows = max(int(rows), 1)
     nbytes = rows * 16
     if nbytes < PLACE_MIN_BYTES or os.environ.get("HJ_PLACEMENT_PROBE", "1") == "0":
         return torch.empty((rows, 2), dtype=torch.int64, device=device)
-    held, best, best_r, draws = [], None, float("inf"), 0
+    good = float(lib.hj_placement_set_good(0.0))
+    torch.cuda.synchronize(device)
+    held, best, best_r, draws, rejected, held_max, low_mem = [], None, float("inf"), 0, 0, 0, False
     for k in range(PLACE_DRAWS):
-        if k > 0 and torch.cuda.mem_get_info(device)[0] < 3 * nbytes:
+        if k > 0 and torch.cuda.mem_get_info(device)[0] < PLACE_SPARE * nbytes:
+            low_mem = True
             break
         t = torch.empty((rows, 2), dtype=torch.int64, device=device)
         r = C.c_double(0.0)
-        check(lib.hj_placement_check(_ptr(t), nbytes, C.byref(r)), "hj_placement_check")
+        with torch.cuda.device(device):
+            check(lib.hj_placement_check(_ptr(t), nbytes, C.byref(r)), "hj_placement_check")
         draws += 1
         if r.value < best_r:
-            if best is not None:
-                held.append(best)
-            best, best_r = t, r.value
+            rej, best, best_r = best, t, r.value
         else:
-            held.append(t)
-        if best_r <= PLACE_GOOD:
+            rej = t
+        if rej is not None:
+            rejected += 1
+            held.append(rej)
+            if len(held) > PLACE_HELD:
+                held.pop(0)
+            held_max = max(held_max, len(held))
+        if best_r <= good:
             break
     _py_place["probes"] += draws
-    _py_place["rejected"] += len(held)
+    _py_place["rejected"] += rejected
+    if best_r > good:
+        _py_place["gave_up"] += 1
+        _py_place["gave_up_low_mem"] += int(low_mem)
+    _py_place["held_max"] = max(_py_place["held_max"], held_max)
     _py_place["last_kept_ratio"] = round(best_r, 3)
     _py_place["worst_kept_ratio"] = max(_py_place["worst_kept_ratio"], round(best_r, 3))
-    if held:
-        del held
+    if rejected:
+        del held, rej
         torch.cuda.empty_cache()   # the rejects go back to the driver, not to torch's cache
     return best
 
 
 def placement_stats():
-    """Row-buffer placement probe counts of this process (hj_placement_stats):
-    draws probed / rejected and the pattern/flat write ratio of the last and
-    the worst buffer kept (~1.0 good, 1.25-1.35 a slow placement)."""
-    pr, rj = C.c_longlong(0), C.c_longlong(0)
+    """Row-buffer placement probe counts of this process (hj_placement_stats_ex):
+    draws probed / rejected, buffers that kept a slow draw (gave_up; of those,
+    gave_up_low_mem: free memory below 3x the buffer stopped the draws), the
+    most rejected draws held at once, and the pattern/flat write ratio of the
+    last and the worst buffer kept (~1.0 good, 1.25-1.35 a slow placement);
+    routed_tuples: the same for the Python-drawn routed-tuple buffers."""
+    out = (C.c_longlong * 5)()
     last, worst = C.c_double(0.0), C.c_double(0.0)
-    lib.hj_placement_stats(C.byref(pr), C.byref(rj), C.byref(last), C.byref(worst))
-    return {"probes": pr.value, "rejected": rj.value, "last_kept_ratio": round(last.value, 3),
-            "worst_kept_ratio": round(worst.value, 3), "routed_tuples": dict(_py_place)}
+    lib.hj_placement_stats_ex(out, C.byref(last), C.byref(worst))
+    return {"probes": out[0], "rejected": out[1], "gave_up": out[2], "gave_up_low_mem": out[3],
+            "held_max": out[4], "last_kept_ratio": round(last.value, 3), "worst_kept_ratio": round(worst.value, 3),
+            "routed_tuples": dict(_py_place)}
 
 
 def partition_of(key: int, nparts: int) -> int:

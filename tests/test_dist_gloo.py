@@ -7,7 +7,6 @@ hashjoin.dist.exchange (the same torch.distributed all-to-all code that runs
 over RCCL on the GPU box), joins locally with the oracle, and rank 0 checks
 that the union of the per-rank results is exactly the global join."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -17,17 +16,20 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# a rank that never reaches its rendezvous (e.g. a port taken between
-# _free_port and init) must fail the test, not hang the suite
+# a rank that never reaches its rendezvous must fail the test, not hang the
+# suite
 pytestmark = pytest.mark.timeout(300, method="thread")
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _rdzv(tmp_path):
+    """A per-test FileStore rendezvous: no TCP port is
+    probed, closed and re-bound, so no other process can take it between the
+    probe and init_process_group."""
+    return "file://" + str(tmp_path / "rdzv")
+
+
+def _init(rank, world, rdzv):
+    dist.init_process_group("gloo", init_method=rdzv, rank=rank, world_size=world)
 
 
 def _route(keys, pays, P):
@@ -39,13 +41,11 @@ def _route(keys, pays, P):
     return torch.from_numpy(np.ascontiguousarray(tuples)), torch.from_numpy(counts)
 
 
-def _worker(rank, world, port, case, outdir):
+def _worker(rank, world, rdzv, case, outdir):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mlir-hashjoin_amd"))
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, rdzv)
     from oracle import pyoracle as O
     from hashjoin.dist import exchange
     NR, NS = case["NR"], case["NS"]
@@ -85,7 +85,7 @@ def _worker(rank, world, port, case, outdir):
 ], ids=["pkfk", "uniform_dups", "tiny", "pieces", "three_ranks_pieces", "four_ranks_dups_pieces"])
 def test_two_rank_exchange_join(case, tmp_path, oracle):
     world = case.get("world", 2)
-    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _rdzv(tmp_path), case, str(tmp_path)), nprocs=world, join=True)
     rs, ss, tot_r, tot_s = [], [], 0, 0
     for k in range(world):
         with np.load(tmp_path / f"rank{k}.npz", allow_pickle=False) as z:
@@ -192,13 +192,11 @@ def _relations(case, rank, world):
     return rk, rp, sk, sp
 
 
-def _dj_worker(rank, world, port, case, outdir):
+def _dj_worker(rank, world, rdzv, case, outdir):
     sys.path.insert(0, HERE)
     sys.path.insert(0, os.path.dirname(HERE))
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mlir-hashjoin_amd"))
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, rdzv)
     from hashjoin.dist import distributed_join
     from test_abi import _np_partition_of
     rk, rp, sk, sp = (torch.from_numpy(x) for x in _relations(case, rank, world))
@@ -282,7 +280,7 @@ def _dj_worker(rank, world, port, case, outdir):
         "folded_one_rank_parts", "folded_8ranks_sub6", "folded_8ranks_product_plan_dups"])
 def test_distributed_join_gloo(case, tmp_path, oracle):
     world = case.get("world", 2)
-    mp.spawn(_dj_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_dj_worker, args=(world, _rdzv(tmp_path), case, str(tmp_path)), nprocs=world, join=True)
     rs, ss = [], []
     for k in range(world):
         with np.load(tmp_path / f"dj{k}.npz", allow_pickle=False) as z:
@@ -303,7 +301,7 @@ def test_distributed_join_flagged_count_raises(case, tmp_path):
     """a probe count with bit 63 set (an internal work list
     overflowed) must raise on every distributed path instead of reading as a
     negative M (a silently truncated or empty result)."""
-    mp.spawn(_dj_worker, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_dj_worker, args=(2, _rdzv(tmp_path), case, str(tmp_path)), nprocs=2, join=True)
 
 
 def test_checked_count_helpers():

@@ -633,3 +633,33 @@ def test_radix_duplicates_across_build_rounds(hj, oracle, wide, dups):
         assert oracle.same_multiset(*o, ex[0].astype(np.int64), ex[1].astype(np.int64))
     assert len(o[0]) == 8
     assert hj.has_duplicates() == dups
+
+
+@pytest.mark.parametrize("wide", [True, False])
+def test_radix_has_duplicates_hot_key_in_oversized_partition(hj, oracle, wide):
+    """has_duplicates() over a build side whose one key repeats 2^17 times in
+    partitions far too large for an LDS table (2 radix bits, ~2^18 rows each,
+    deferred to k_join's rounds): the rounds' own build flags the repeat and
+    radix_detect's count-only self-join of the deferred partitions is then
+    skipped (run, it would walk every copy's chain past ~2560
+    copies per round, ~m^2 steps) -- correct, and answered in well under a
+    second."""
+    import time
+    n, hot = 1 << 20, 1 << 17
+    rng = np.random.default_rng(4242 + (1 if wide else 0))
+    rk = rng.choice(np.arange(1, 1 << 30, dtype=np.int64), size=n, replace=False)
+    rk[rng.choice(n, size=hot, replace=False)] = 7
+    sk = rk[rk != 7][:8].copy()     # 8 probe rows, none with the hot key
+    rp = np.arange(n, dtype=np.int64) * 3 + 1
+    sp = np.arange(len(sk), dtype=np.int64) + 5
+    if wide:
+        o = run(hj, rk, rp, sk, sp, 2)
+        assert oracle.same_multiset(*o, *oracle.nested_loop_i64(rk, rp, sk, sp))
+    else:
+        o = run(hj, rk.astype(np.int32), None, sk.astype(np.int32), None, 2)
+        assert len(o[0]) == 8 and np.array_equal(np.sort(sk.astype(np.int64)), np.sort(rk[o[0]]))
+    assert len(o[0]) == 8
+    t0 = time.perf_counter()
+    assert hj.has_duplicates()
+    assert time.perf_counter() - t0 < 5.0
+
