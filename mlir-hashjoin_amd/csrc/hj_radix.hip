@@ -3085,13 +3085,17 @@ constexpr int kGrpNT = 512, kGrpRI = 3, kGrpSI = 8;
 constexpr int kGrpWideRI = 3, kGrpWideSI = 3, kGrpWidePerCU = 2;
 constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 x 16 B)
 // i32 rows: k_join_b over 8192 slots (keys and row ids apart: 64 KiB), 768
-// threads x 3 build + 5 probe rows, 6 waves per SIMD, 2 workgroups per CU;
+// threads x 4 build + 5 probe rows, 6 waves per SIMD, 2 workgroups per CU;
 // plan partitions of ~4096 rows (log2 of twice the average build rows).
 // Round 5: 3 + 5 instead of 4 + 4 -- a REF-B partition (~3050 rows, ~48
 // runs) takes two build rounds instead of one or two, but its probe rows
 // one sub-chunk instead of two, and a sub-chunk (scan, output atomic, three
 // barriers) costs more than a build round: REF-B join 0.766 -> 0.695 ms
 // (profiles/r05/r05zq_narrow_3p5_ab.jsonl; 5 + 3 0.87, 2 + 6 / 3 + 6 spill).
+// Round 6: 4 + 5 (80 VGPRs, no spill): most REF-B partitions now take one
+// build round as well -- join 0.695-0.697 -> 0.687 ms, step -0.5 % in three
+// alternating pairs (profiles/r06/r06o_narrow_4p5_ab.jsonl); 4 + 6, 5 + 5
+// and 4 + 7 spill 24 / 12 / 60 B.
 // REF-B's join (profiles/r03_narrow_shapes.txt; the other shapes live on in
 // micro/ only): k_join_u over 8192 slots 1.16 ms; k_join_b over 4096 slots
 // 768 x 3+3 0.92, 512 x 5+4 at 3 per CU 0.96, 512 x 5+3 at 4 per CU 1.35 and
@@ -3101,7 +3105,7 @@ constexpr int kTableLog = 12;   // LDS table slots of the int64-row joins (2^12 
 // (micro/runs_micro.hip), so shapes with larger rounds were tried
 // (profiles/r04_narrow_rounds.txt): 640 x 5+5 at 5 waves per SIMD 1.31 ms,
 // 640 x 6+6 1.24, 896 x 4+4 at 7 per SIMD 1.08, against 0.82 for this one.
-constexpr int kNarrowNT = 768, kNarrowRI = 3, kNarrowSI = 5, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
+constexpr int kNarrowNT = 768, kNarrowRI = 4, kNarrowSI = 5, kNarrowWPS = 6, kNarrowPerCU = 2, kTableLogNarrow = 13,
               kPlanLogNarrow = 13;
 
 int cu_count() {
