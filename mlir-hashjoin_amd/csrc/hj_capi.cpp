@@ -132,6 +132,7 @@ struct hj_ctx {
     int radix_bits = 0;                // 0: planner chooses
     int used = 0;                      // HJ_STRATEGY_GLOBAL / _RADIX of the current build
     bool dual = false;                 // global build whose R is ALSO radix-partitioned (probe-time choice)
+    int64_t probe_hint = -1;           // expected probe rows (hj_ctx_probe_hint; < 0 unknown)
     int probe_used = -1;               // strategy of the last probe (-1: none since the build)
     // radix-join workspace (hj_radix.hip)
     hj::RadixPlan plan;
@@ -548,7 +549,10 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     // EXACT copies it has just taken of its inputs)
     if (c->host_building) c->memo.valid = false;
     else c->memo.invalidate();
-    c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows;
+    // (a probe side known to stay below the radix probe's threshold never
+    // takes the partitioned R)
+    c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows &&
+              (c->probe_hint < 0 || c->probe_hint >= kRadixProbeMinRows);
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
         // per partition in LDS at probe time)
@@ -1083,7 +1087,10 @@ int host_join(hj_ctx *c, int layout, const HostRel &r, const HostRel &s, HostMod
         HJ_TRY(upload_rel(c, layout, s, ds_buf, &ssrc));
     }
     c->host_building = true;
+    const int64_t hint = c->probe_hint;
+    c->probe_hint = s.n;
     const int brc = do_build(c, layout, rsrc, st);
+    c->probe_hint = hint;
     c->host_building = false;
     HJ_TRY(brc);
     if (mode != kHostCount) {
@@ -1539,6 +1546,12 @@ int hj_ctx_set_radix_bits(hj_ctx *c, int bits) {
 int hj_ctx_strategy_used(const hj_ctx *c) {
     if (!c || c->layout < 0) return 0;
     return c->probe_used >= 0 ? c->probe_used : c->used;
+}
+
+int hj_ctx_probe_hint(hj_ctx *c, int64_t probe_rows) {
+    if (!c) HJ_FAIL(HJ_ERR_ARG, "null context");
+    c->probe_hint = probe_rows < 0 ? -1 : probe_rows;
+    return HJ_OK;
 }
 
 int hj_ctx_reserve_probe(hj_ctx *c, int64_t max_probe_rows, int key_bits) {

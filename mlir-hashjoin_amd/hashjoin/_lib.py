@@ -64,6 +64,7 @@ def _load():
         "hj_ctx_timing_accumulate": (_int, [_vp, _int]),
         "hj_ctx_timing_totals": (_int, [_vp, C.POINTER(C.c_float), C.POINTER(C.c_longlong)]),
         "hj_ctx_reserve_probe": (_int, [_vp, _i64, _int]),
+        "hj_ctx_probe_hint": (_int, [_vp, _i64]),
         "hj_ctx_set_strategy": (_int, [_vp, _int]),
         "hj_ctx_strategy_used": (_int, [_vp]),
         "hj_ctx_set_radix_bits": (_int, [_vp, _int]),

@@ -75,6 +75,12 @@ class HashJoin:
     def reserve_probe(self, num_tuples, key_bits=64):
         check(lib.hj_ctx_reserve_probe(self._ctx, int(num_tuples), int(key_bits)), "hj_ctx_reserve_probe")
 
+    def probe_hint(self, num_tuples):
+        """The probe side's expected rows, given before the build (None or < 0:
+        unknown).  AUTO spares a mid-size build the radix partition it keeps
+        only for probe sides of >= 2^24 rows (hj_ctx_probe_hint)."""
+        check(lib.hj_ctx_probe_hint(self._ctx, -1 if num_tuples is None else int(num_tuples)), "hj_ctx_probe_hint")
+
     def set_strategy(self, name, radix_bits=0):
         """'auto' | 'global' (one HBM table) | 'radix' (partitioned, LDS tables);
         radix_bits > 0 fixes the partition count to 2^radix_bits."""
@@ -342,7 +348,11 @@ class HashJoin:
         """The @main join (join_v2.mlir:646-696) on device tensors: build, then
         probe into an output sized optimistically (|S| rows, or `capacity`),
         re-probing once at the exact M if that was too small."""
-        self.build_table(rkey, rpay, stream=stream)
+        self.probe_hint(skey.numel())
+        try:
+            self.build_table(rkey, rpay, stream=stream)
+        finally:
+            self.probe_hint(None)
         dt = torch.int64 if rkey.dtype == torch.int64 else torch.int32
         cap = max(1, skey.numel() if capacity is None else int(capacity))
         for _ in range(2):

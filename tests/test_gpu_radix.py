@@ -211,6 +211,37 @@ def test_auto_probe_time_strategy(hj):
     assert res == {1 << 20: "global", 1 << 24: "radix"}
 
 
+def test_auto_probe_hint(hj):
+    """hj_ctx_probe_hint: a probe side known to stay below 2^24 rows spares a
+    [2^18, 2^21)-row AUTO build its radix partition (no plan); a later, larger
+    probe still joins -- through the global table, with the pairs of a
+    forced-global join."""
+    nr, ns = 1 << 18, 1 << 24
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EEE, nr, ns, 0.95)
+    hj.set_strategy("auto")
+    try:
+        hj.probe_hint(None)
+        hj.build_table(rk, rp)
+        assert hj.radix_plan   # unknown probe side: R partitioned as well
+        hj.probe_hint(1 << 20)
+        hj.build_table(rk, rp)
+        assert not hj.radix_plan
+        out_r = torch.empty(ns, dtype=torch.int64, device="cuda")
+        out_s = torch.empty_like(out_r)
+        m = int(hj.probe_relation(sk, sp, out_r, out_s).item())
+        assert hj.strategy_used == "global"
+        hj.probe_hint(None)
+        hj.set_strategy("global")
+        g_r, g_s = hj.join(rk, rp, sk, sp)
+        assert m == g_r.numel()
+        o_r, o_s = out_r[:m], out_s[:m]
+        order, gorder = torch.argsort(o_s), torch.argsort(g_s)
+        assert torch.equal(o_r[order], g_r[gorder]) and torch.equal(o_s[order], g_s[gorder])
+    finally:
+        hj.probe_hint(None)
+        hj.set_strategy("auto")
+
+
 @pytest.mark.parametrize("bits", [9, 17])
 def test_radix_hot_key_tiles_i32(hj, oracle, bits):
     """The same skew on the reference types (i32 keys, row-id payloads)."""
