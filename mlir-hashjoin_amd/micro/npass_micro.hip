@@ -78,9 +78,6 @@ int main() {
     P(2, "synthetic rows (no loads)");
     P(4, "no row stores");
     P(6, "synthetic rows, no stores");
-    P(16, "static buffer stores");
-    P(0, "product (2)");
-    P(16, "static buffer stores (2)");
 #undef P
     u64 *prof;
     CK(hipMalloc(&prof, grid * 8 * sizeof(u64)));

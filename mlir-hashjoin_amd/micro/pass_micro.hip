@@ -99,9 +99,6 @@ int main(int argc, char **argv) {
             P(2, "synthetic rows");
             P(4, "no row stores");
             P(6, "synthetic rows, no stores");
-            P(16, "static buffer stores");
-            P(0, "k_pass (2)");
-            P(16, "static buffer stores (2)");
 #undef P
             // phase times (cycles of s_memtime, summed over a workgroup's tiles, mean over workgroups)
             u64 *prof;
