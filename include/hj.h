@@ -94,9 +94,10 @@ int hj_ctx_set_radix_bits(hj_ctx *ctx, int bits);
  * side of >= 2^24 rows then takes the radix join. */
 int hj_ctx_strategy_used(const hj_ctx *ctx);
 /* The probe side's expected rows, given before the build (< 0: unknown, the
- * default).  AUTO: a hint below 2^24 rows spares a [2^18, 2^21)-row build the
- * radix partition it keeps only for such probe sides (2^20 x 2^20: 0.21 ->
- * 0.15 ms per join).  A later, larger probe still joins correctly, through
+ * default).  AUTO with a [2^18, 2^21)-row build side then builds ONE
+ * strategy instead of both: radix from 2^24 hinted probe rows on (2^22 for
+ * build sides of >= 2^20 rows), else the global table (2^20 x 2^20: 0.21 ->
+ * 0.15 ms per join; 2^20 x 2^22: 0.24 -> 0.20).  A later, larger probe still joins correctly, through
  * the global table.  HashJoin.join and the host memref entry points set it. */
 int hj_ctx_probe_hint(hj_ctx *ctx, int64_t probe_rows);
 /* GLOBAL: slot capacity of the table (power of two, >= 2 x build rows);

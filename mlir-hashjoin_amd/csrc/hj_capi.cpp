@@ -100,6 +100,13 @@ constexpr int64_t kRadixMinRows = 1ll << 21;
 // C2 26.4 ms) while partition + LDS join streams (C2 19.7 ms).
 constexpr int64_t kDualMinBuildRows = 1ll << 18;
 constexpr int64_t kRadixProbeMinRows = 1ll << 24;
+// A probe side KNOWN before the build (hj_ctx_probe_hint) takes the radix
+// join alone from these many rows on: 2^22 for build sides of >= 2^20 rows,
+// else 2^24 (round 6, profiles/r06/r06sc_strategy_cross.txt: 2^20 x 2^22
+// radix 0.204 ms, global 0.233; 2^19 x 2^21 global 0.134, radix 0.166).
+// Without a hint the dual build keeps kRadixProbeMinRows: its global table
+// is already paid for, and its global probe beats partitioning S below 2^24.
+inline int64_t radix_probe_min_rows(int64_t n_build) { return n_build >= (1ll << 20) ? 1ll << 22 : kRadixProbeMinRows; }
 
 struct Buf {
     void *p = nullptr;
@@ -527,7 +534,9 @@ hj::RadixWork radix_work(hj_ctx *c) {
 
 int choose_strategy(const hj_ctx *c, int64_t n_build) {
     if (c->strategy == HJ_STRATEGY_GLOBAL || c->strategy == HJ_STRATEGY_RADIX) return c->strategy;
-    return n_build >= kRadixMinRows ? HJ_STRATEGY_RADIX : HJ_STRATEGY_GLOBAL;
+    if (n_build >= kRadixMinRows) return HJ_STRATEGY_RADIX;
+    if (n_build >= kDualMinBuildRows && c->probe_hint >= radix_probe_min_rows(n_build)) return HJ_STRATEGY_RADIX;
+    return HJ_STRATEGY_GLOBAL;
 }
 
 int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
@@ -549,10 +558,9 @@ int do_build(hj_ctx *c, int layout, const hj::SrcDev &src, hipStream_t st) {
     // EXACT copies it has just taken of its inputs)
     if (c->host_building) c->memo.valid = false;
     else c->memo.invalidate();
-    // (a probe side known to stay below the radix probe's threshold never
-    // takes the partitioned R)
+    // (a known probe side settled the strategy in choose_strategy: no dual)
     c->dual = c->used == HJ_STRATEGY_GLOBAL && c->strategy == HJ_STRATEGY_AUTO && src.n >= kDualMinBuildRows &&
-              (c->probe_hint < 0 || c->probe_hint >= kRadixProbeMinRows);
+              c->probe_hint < 0;
     if (c->used == HJ_STRATEGY_RADIX || c->dual) {
         // build = radix-partition R by the top key-hash bits (tables are built
         // per partition in LDS at probe time)

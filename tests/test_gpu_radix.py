@@ -694,3 +694,24 @@ def test_radix_has_duplicates_hot_key_in_oversized_partition(hj, oracle, wide):
     assert hj.has_duplicates()
     assert time.perf_counter() - t0 < 5.0
 
+
+
+def test_auto_probe_threshold_by_build_size(hj):
+    """AUTO's probe-time choice for a [2^18, 2^21)-row build: from 2^22 probe
+    rows on the radix join when the build side has >= 2^20 rows (2^24
+    below that) -- same pairs as a forced-global join."""
+    nr, ns = 1 << 20, 1 << 22
+    rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EEF, nr, ns, 0.9)
+    hj.set_strategy("auto")
+    try:
+        o_r, o_s = hj.join(rk, rp, sk, sp)
+        assert hj.strategy_used == "radix"
+        small_r, small_s = hj.join(rk, rp, sk[:ns // 2], sp[:ns // 2])
+        assert hj.strategy_used == "global"
+        hj.set_strategy("global")
+        g_r, g_s = hj.join(rk, rp, sk, sp)
+        assert o_r.numel() == g_r.numel()
+        order, gorder = torch.argsort(o_s), torch.argsort(g_s)
+        assert torch.equal(o_r[order], g_r[gorder]) and torch.equal(o_s[order], g_s[gorder])
+    finally:
+        hj.set_strategy("auto")
