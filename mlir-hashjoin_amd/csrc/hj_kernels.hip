@@ -170,6 +170,13 @@ __global__ __launch_bounds__(kBlock) void k_build(TableDev t, SrcDev src) {
 // ------------------------------------------------------------------ probe tiles
 // A probe tile is kProbeItems * kBlock rows: tile q = rows [q * kTile, ...).
 constexpr int kProbeTile = kBlock * kProbeItems;
+#ifndef HJ_LDS_TABLE_BYTES
+#define HJ_LDS_TABLE_BYTES 65536
+#endif
+// global tables up to this size are probed from LDS (k_probe<..., LDS>);
+// kLdsPerCu: the LDS the copies of one CU's workgroups may take together
+constexpr int kLdsTableBytes = HJ_LDS_TABLE_BYTES;
+constexpr int kLdsPerCu = 128 * 1024;
 
 template <int L, int FORM>
 __device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned long long q, int i, Tuple &tp) {
@@ -201,7 +208,12 @@ __device__ __forceinline__ bool probe_row(const SrcDev &src, unsigned long long 
 // flush; more than kStage matches spill straight to global (the v2 overflow
 // path, :539-549).  The cursor counts every match, so a caller whose
 // capacity was too small still learns the exact M (rows past cap dropped).
-template <int L, int FORM, bool WRITE>
+//
+// LDS (small tables, <= kLdsTableBytes): each workgroup first copies the
+// whole table into LDS and the fast path reads its slots there; the probes
+// of a table that fits one XCD's L2 were random L2 reads (~82-96 G/s), well
+// below the rate the probe side streams at (profiles/r06/r06sr_small_build_sides.txt).
+template <int L, int FORM, bool WRITE, bool LDS = false>
 __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev out, unsigned *slow,
                                                   unsigned long long slow_cap) {
     using LY = Lay<L>;
@@ -211,8 +223,19 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
     __shared__ unsigned long long st_base;
     __shared__ unsigned long long wsum[NW];
     __shared__ unsigned s_cw[kProbeItems * NW];
+    extern __shared__ ulonglong2 s_tab[];
 
     const slot_t *sl = (const slot_t *)t.slots;
+    if constexpr (LDS) {
+        const unsigned long long n16 = (t.mask + 1) * sizeof(slot_t) / 16;
+        const ulonglong2 *g16 = (const ulonglong2 *)t.slots;
+        for (unsigned long long j = threadIdx.x; j < n16; j += kBlock) s_tab[j] = g16[j];
+        __syncthreads();
+    }
+    auto slot_at = [&](unsigned long long h) -> slot_t {
+        if constexpr (LDS) return ((const slot_t *)s_tab)[h];
+        else return sl[h];
+    };
     const bool unique = (__hip_atomic_load(&t.meta[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned long long nt = (unsigned long long)((src.n + kProbeTile - 1) / kProbeTile);
@@ -241,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
 #pragma unroll
         for (int i = 0; i < kProbeItems; ++i) {
             H[i] = slot_of(K[i], t.shift);
-            if (V[i]) S[i] = sl[H[i]];
+            if (V[i]) S[i] = slot_at(H[i]);
         }
         unsigned found = 0;
         unsigned long long RP[kProbeItems];
@@ -255,7 +278,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
             unsigned long long hh = H[i];
             while (!LY::empty(sv) && LY::key(sv) != K[i]) {
                 hh = (hh + 1) & t.mask;
-                sv = sl[hh];
+                sv = slot_at(hh);
             }
             if (!LY::empty(sv)) {
                 found |= 1u << i;
@@ -914,16 +937,30 @@ hipError_t launch_probe(const TableDev &t, int layout, const SrcDev &src, const 
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const unsigned tiles = grid_for(src.n, kProbeTile);
-    const unsigned g = tiles;   // one block per tile
     const unsigned gs = tiles < (unsigned)(cus * 8) ? tiles : (unsigned)(cus * 8);
+    // a table of <= kLdsTableBytes: every workgroup copies it into LDS once
+    // and strides over the tiles (as many workgroups as LDS lets a CU hold)
+    const size_t tbytes = (size_t)(t.mask + 1) * (layout == kWide ? 16 : 8);
+    const bool lds = tbytes <= (size_t)kLdsTableBytes && tbytes >= 16;
+    unsigned per_cu = lds ? (unsigned)(kLdsPerCu / tbytes) : 1u;
+    if (per_cu > 8) per_cu = 8;
+    if (per_cu < 1) per_cu = 1;
+    const unsigned gl = tiles < (unsigned)cus * per_cu ? tiles : (unsigned)cus * per_cu;
+    const unsigned g = lds ? gl : tiles;   // (global table: one block per tile)
 #define HJ_PROBE(L, F)                                                                                        \
     do {                                                                                                      \
         if (count_only) {                                                                                     \
-            hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap); \
+            if (lds)                                                                                          \
+                hipLaunchKernelGGL((k_probe<L, F, false, true>), dim3(g), dim3(kBlock), tbytes, st, t, src,   \
+                                   out, slow, cap);                                                           \
+            else hipLaunchKernelGGL((k_probe<L, F, false>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap); \
             hipLaunchKernelGGL((k_probe_slow<L, F, false>), dim3(gs), dim3(kBlock), 0, st, t, src, out,       \
                                (const unsigned *)slow, cap);                                                  \
         } else {                                                                                              \
-            hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap);  \
+            if (lds)                                                                                          \
+                hipLaunchKernelGGL((k_probe<L, F, true, true>), dim3(g), dim3(kBlock), tbytes, st, t, src,    \
+                                   out, slow, cap);                                                           \
+            else hipLaunchKernelGGL((k_probe<L, F, true>), dim3(g), dim3(kBlock), 0, st, t, src, out, slow, cap); \
             hipLaunchKernelGGL((k_probe_slow<L, F, true>), dim3(gs), dim3(kBlock), 0, st, t, src, out,        \
                                (const unsigned *)slow, cap);                                                  \
         }                                                                                                     \

@@ -1,0 +1,73 @@
+"""Global tables small enough to live in LDS (k_probe<..., LDS>, tables of
+<= 64 KiB: int64 builds of <= 2048 rows, i32 builds of <= 4096 rows) against
+the oracle: unique and repeated build keys, INT64_MIN probe keys (their
+tiles take the general path), count-only, i32 reference types, and the sizes
+either side of the LDS limit."""
+import numpy as np
+import pytest
+import torch
+
+from hashjoin import HashJoin
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hj():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    h = HashJoin(0)
+    h.set_strategy("global")
+    yield h
+    h.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def join(hj, rk, rp, sk, sp):
+    if rk.dtype == np.int32:
+        o_r, o_s = hj.join(dev(rk), None, dev(sk), None)
+    else:
+        o_r, o_s = hj.join(dev(rk), dev(rp), dev(sk), dev(sp))
+    torch.cuda.synchronize()
+    assert hj.strategy_used == "global"
+    return o_r.cpu().numpy().astype(np.int64), o_s.cpu().numpy().astype(np.int64)
+
+
+@pytest.mark.parametrize("nr", [1, 100, 1000, 1024, 2048, 3000])   # 3000: 8192 slots, past the LDS limit
+def test_small_table_pkfk(hj, oracle, nr):
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(nr, nr, 1 << 20, 0.8)
+    o = join(hj, rk, rp, sk, sp)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=max(1, nr // 4)))
+
+
+def test_small_table_repeated_build_keys(hj, oracle):
+    rk, rp = oracle.gen_uniform_i64(61, 1, 1, 300, 1000)
+    sk, sp = oracle.gen_uniform_i64(61, 2, 1, 400, 1 << 18)
+    o = join(hj, rk, rp, sk, sp)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=100))
+
+
+def test_small_table_int64_min_probe_keys(hj, oracle):
+    I64_MIN = -(1 << 63)
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(62, 1500, 1 << 19, 0.9)
+    rk[::211] = I64_MIN
+    sk[::1777] = I64_MIN
+    o = join(hj, rk, rp, sk, sp)
+    assert oracle.same_multiset(*o, *oracle.nested_loop_i64(rk, rp, sk[:1 << 19], sp[:1 << 19]))
+
+
+def test_small_table_count_only(hj, oracle):
+    rk, rp, sk, sp = oracle.gen_pkfk_i64(63, 700, 1 << 20, 0.6)
+    hj.build_table(dev(rk), dev(rp))
+    er, _ = oracle.chained_join_i64(rk, rp, sk, sp, H=100)
+    assert hj.count_rows(dev(sk)) == len(er)
+
+
+@pytest.mark.parametrize("nr", [1000, 4000, 5000])   # i32: 8192 slots x 8 B = 64 KiB; 5000: past it
+def test_small_table_i32(hj, oracle, nr):
+    r = oracle.gen_uniform_i32(64, 1, 1, 1 << 20, nr)
+    s = oracle.gen_uniform_i32(64, 2, 1, 1 << 20, 1 << 20)
+    o = join(hj, r, None, s, None)
+    assert oracle.same_multiset(*o, *oracle.chained_join_i32(r, s, H=max(1, nr // 4)))

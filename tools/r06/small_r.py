@@ -12,7 +12,7 @@ import torch  # noqa: E402
 import hashjoin  # noqa: E402
 
 ns = 1 << 26
-for lg in (10, 12, 14, 16, 18):
+for lg in (10, 11, 12, 14, 16, 18):
     nr = 1 << lg
     rk, rp, sk, sp = hashjoin.gen_pkfk(0x5EED, nr, ns, 1.0)
     out_r = torch.empty(ns, dtype=torch.int64, device="cuda")
