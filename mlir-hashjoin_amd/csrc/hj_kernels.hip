@@ -251,12 +251,16 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
             P[i] = tp.p;
             has_null |= V[i] && LY::null_key(K[i]);
         }
-        if (!unique || __syncthreads_or(has_null ? 1 : 0)) {
-            // general path: k_probe_slow takes this tile
+        // general path (k_probe_slow takes the tile): a null probe key, or
+        // -- with repeated build keys -- a row with more than one match
+        auto to_slow = [&]() {
             if (threadIdx.x == 0) {
                 const unsigned long long j = atomicAdd(&t.meta[3], 1ull);
                 if (j < slow_cap) slow[j] = (unsigned)q;   // (sized so it always is; else k_probe_slow flags the count)
             }
+        };
+        if (__syncthreads_or(has_null ? 1 : 0)) {
+            to_slow();
             continue;
         }
         slot_t S[kProbeItems];
@@ -283,6 +287,35 @@ __global__ __launch_bounds__(kBlock) void k_probe(TableDev t, SrcDev src, OutDev
             if (!LY::empty(sv)) {
                 found |= 1u << i;
                 RP[i] = LY::pay(sv);
+            }
+        }
+        if (!unique) {
+            // repeated build keys: a matched row walks on to EMPTY; a second
+            // copy of its key sends the tile to the general path (a few
+            // repeated keys used to send every tile there: i32 2^12 random
+            // build keys, 3.2 ms against 0.6 without a repeat,
+            // profiles/r06/r06lu_lds_table_probe_ab.txt)
+            bool multi = false;
+#pragma unroll
+            for (int i = 0; i < kProbeItems; ++i) {
+                if (!((found >> i) & 1u)) continue;
+                unsigned long long hh = slot_of(K[i], t.shift);
+                slot_t sv = slot_at(hh);
+                while (!LY::empty(sv) && LY::key(sv) != K[i]) {   // (back to the first copy)
+                    hh = (hh + 1) & t.mask;
+                    sv = slot_at(hh);
+                }
+                hh = (hh + 1) & t.mask;
+                sv = slot_at(hh);
+                while (!LY::empty(sv) && !multi) {
+                    multi = LY::key(sv) == K[i];
+                    hh = (hh + 1) & t.mask;
+                    sv = slot_at(hh);
+                }
+            }
+            if (__syncthreads_or(multi ? 1 : 0)) {
+                to_slow();
+                continue;
             }
         }
         if constexpr (!WRITE) {

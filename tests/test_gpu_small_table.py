@@ -71,3 +71,27 @@ def test_small_table_i32(hj, oracle, nr):
     s = oracle.gen_uniform_i32(64, 2, 1, 1 << 20, 1 << 20)
     o = join(hj, r, None, s, None)
     assert oracle.same_multiset(*o, *oracle.chained_join_i32(r, s, H=max(1, nr // 4)))
+
+
+@pytest.mark.parametrize("nr,wide", [(1500, True), (4000, True), (3000, False), (20000, False)])
+def test_few_repeated_build_keys(hj, oracle, nr, wide):
+    """A handful of repeated build keys: only the tiles whose rows meet one go
+    to the general path (every other tile keeps the fast path) -- exact."""
+    rng = np.random.default_rng(nr)
+    if wide:
+        rk, rp = oracle.gen_uniform_i64(nr, 1, 1, 1 << 40, nr)
+        rk[nr - 5:] = rk[:5]                      # five keys twice
+        sk, sp = oracle.gen_uniform_i64(nr, 2, 1, 1 << 40, 1 << 20)
+        idx = rng.integers(0, nr, 1 << 18)
+        sk[:1 << 18] = rk[idx]                    # a quarter of S hits R
+        sk[rng.integers(0, 1 << 20, 40)] = rk[0]  # forty rows meet a repeated key
+        o = join(hj, rk, rp, sk, sp)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i64(rk, rp, sk, sp, H=max(1, nr // 4)))
+    else:
+        r = oracle.gen_uniform_i32(nr, 1, 1, 1 << 30, nr)
+        r[nr - 5:] = r[:5]
+        s = oracle.gen_uniform_i32(nr, 2, 1, 1 << 30, 1 << 20)
+        s[:1 << 18] = r[rng.integers(0, nr, 1 << 18)]
+        s[rng.integers(0, 1 << 20, 40)] = r[0]
+        o = join(hj, r, None, s, None)
+        assert oracle.same_multiset(*o, *oracle.chained_join_i32(r, s, H=max(1, nr // 4)))
