@@ -453,9 +453,6 @@ def main():
     last = {}
 
     if not use_dist:
-        # the probe side's size is known up front (as HashJoin.join passes
-        # it): AUTO builds the one strategy it will probe with
-        hj.probe_hint(NS)
         hj.allocate_hash_table(NR, 64 if wide else 32)
         hj.build_table(rk, rp)
         hj.reserve_probe(NS, 64 if wide else 32)
